@@ -1,0 +1,434 @@
+/*
+ * marf_oracle.c -- CPU restatement of the reference's planar-warp prologue.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker; the product
+ * (masking-bundle-adjusting-neural-radiance-fields_amd/) never links or calls it.
+ *
+ * Restates, in plain C with the exact fp32 operation order of the reference run on
+ * PyTorch-CPU (pinned bit-for-bit against the tests/golden fixtures generated from the
+ * reference itself by tests/golden/make_golden.py):
+ *   - Lie.sl3_to_SL3            warp.py:98-106  (torch.linalg.matrix_exp, fp32)
+ *   - matrix_exp backward        (torch: exp of [[A^T, G],[0, A^T]], upper-right block)
+ *   - Warp.get_normalized_pixel_grid warp.py:33-68
+ *   - Warp.warp_grid             warp.py:70-81  (bmm as an FMA chain + divide)
+ *   - NeuralImageFunction.positional_encoding model/planar.py:451-471
+ *
+ * matrix_exp follows torch's implementation (Bader/Blanes/Casas optimized Taylor):
+ *   batch >= 2  -> always degree 18 + scaling & squaring;
+ *   batch == 1  -> degree chosen from the 1-norm (1,2,4,8,12,18).
+ * Linear combinations of matrix powers accumulate with FMA (out = fma(A_j, c_j, out),
+ * out starting at 0); small matrix products accumulate with separate mul and add,
+ * acc starting at 0.  Both verified bitwise against torch 2.10 CPU.
+ *
+ * Build: gcc -O2 -ffp-contract=off -fno-fast-math -shared -fPIC (see oracle/Makefile).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#define MAXN 6
+
+/* ---------------------------------------------------------------- matrix exp */
+
+static void mm_plain(const float* X, const float* Y, float* R, int n) {
+    float tmp[MAXN * MAXN];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            float acc = 0.0f;
+            for (int k = 0; k < n; ++k) {
+                float p = X[i * n + k] * Y[k * n + j];
+                acc = acc + p;
+            }
+            tmp[i * n + j] = acc;
+        }
+    memcpy(R, tmp, sizeof(float) * n * n);
+}
+
+/* out = sum_j c[j] * As[j], out starting at 0, FMA accumulation (torch
+ * _compute_linear_combination CPU kernel). */
+static void lincomb(const float* const* As, const float* c, int m, float* out, int n) {
+    float tmp[MAXN * MAXN];
+    for (int e = 0; e < n * n; ++e) {
+        float acc = 0.0f;
+        for (int j = 0; j < m; ++j) acc = fmaf(As[j][e], c[j], acc);
+        tmp[e] = acc;
+    }
+    memcpy(out, tmp, sizeof(float) * n * n);
+}
+
+static void eye(float* I, int n) {
+    memset(I, 0, sizeof(float) * n * n);
+    for (int i = 0; i < n; ++i) I[i * n + i] = 1.0f;
+}
+
+static void add_inplace(float* X, const float* Y, int n) {
+    for (int e = 0; e < n * n; ++e) X[e] = X[e] + Y[e];
+}
+
+static const double B18[5][5] = {
+    {0., -1.00365581030144618291e-01, -8.02924648241156932449e-03, -8.92138498045333711011e-04, 0.},
+    {0., 3.97849749499645077844e-01, 1.36783778460411720168e+00, 4.98289622525382669416e-01,
+     -6.37898194594723280150e-04},
+    {-1.09676396052962061844e+01, 1.68015813878906206114e+00, 5.71779846478865511061e-02,
+     -6.98210122488052056106e-03, 3.34975017086070470649e-05},
+    {-9.04316832390810593223e-02, -6.76404519071381882256e-02, 6.75961301770459654925e-02,
+     2.95552570429315521194e-02, -1.39180257516060693404e-05},
+    {0., 0., -9.23364619367118555360e-02, -1.69364939002081722752e-02, -1.40086798182036094347e-05}};
+
+static const double B12[4][4] = {
+    {9.0198e-16, 0.46932117595418237389, -0.20099424927047284052, -0.04623946134063071740},
+    {5.31597895759871264183, 1.19926790417132231573, 0.01179296240992997031, 0.01108844528519167989},
+    {0.18188869982170434744, 0.05502798439925399070, 0.09351590770535414968, 0.00610700528898058230},
+    {-2.0861320e-13, -0.13181061013830184015, -0.02027855540589259079, -0.00675951846863086359}};
+
+static void T1(const float* A, float* E, int n) {
+    float I[MAXN * MAXN];
+    eye(I, n);
+    for (int e = 0; e < n * n; ++e) E[e] = I[e] + A[e];
+}
+
+static void T2(const float* A, float* E, int n) {
+    float I[MAXN * MAXN], A2[MAXN * MAXN];
+    eye(I, n);
+    mm_plain(A, A, A2, n);
+    for (int e = 0; e < n * n; ++e) {
+        float h = A2[e] / 2.0f;
+        E[e] = (I[e] + A[e]) + h;
+    }
+}
+
+static void T4(const float* A, float* E, int n) {
+    float I[MAXN * MAXN], A2[MAXN * MAXN], L[MAXN * MAXN], P[MAXN * MAXN];
+    eye(I, n);
+    mm_plain(A, A, A2, n);
+    const float* as3[3] = {I, A, A2};
+    const float c3[3] = {(float)(1 / 2.0), (float)(1 / 6.0), (float)(1 / 24.0)};
+    lincomb(as3, c3, 3, L, n);
+    mm_plain(A2, L, P, n);
+    const float* as4[4] = {I, A, A2, P};
+    const float c4[4] = {1.0f, 1.0f, 0.0f, 1.0f};
+    lincomb(as4, c4, 4, E, n);
+}
+
+static void T8(const float* A, float* E, int n) {
+    const float sqrt_177 = 0.1330413469565007072504e+2;
+    const float x3 = 2. / 3.;
+    const float x1 = x3 * ((1. + sqrt_177) / 88.);
+    const float x2 = x3 * ((1. + sqrt_177) / 352.);
+    const float x4 = (-271. + 29. * sqrt_177) / (315. * x3);
+    const float x5 = (-11. + 11. * sqrt_177) / (1260. * x3);
+    const float x6 = (-99. + 11. * sqrt_177) / (5040. * x3);
+    const float x7 = (89. - sqrt_177) / (5040. * x3);
+    const float y2 = (857. - 58. * sqrt_177) / 630.;
+    float I[MAXN * MAXN], A2[MAXN * MAXN], A4[MAXN * MAXN], A8[MAXN * MAXN], L1[MAXN * MAXN],
+        L2[MAXN * MAXN];
+    eye(I, n);
+    mm_plain(A, A, A2, n);
+    {
+        const float* as[2] = {A, A2};
+        const float c[2] = {x1, x2};
+        lincomb(as, c, 2, L1, n);
+        mm_plain(A2, L1, A4, n);
+    }
+    {
+        const float* asa[2] = {A2, A4};
+        const float ca[2] = {x3, 1.0f};
+        lincomb(asa, ca, 2, L1, n);
+        const float* asb[4] = {I, A, A2, A4};
+        const float cb[4] = {x4, x5, x6, x7};
+        lincomb(asb, cb, 4, L2, n);
+        mm_plain(L1, L2, A8, n);
+    }
+    const float* as5[5] = {I, A, A2, A4, A8};
+    const float c5[5] = {1.0f, 1.0f, y2, 0.0f, 1.0f};
+    lincomb(as5, c5, 5, E, n);
+}
+
+static void T12(const float* A, float* E, int n) {
+    float I[MAXN * MAXN], A2[MAXN * MAXN], A3[MAXN * MAXN];
+    float Bs[4][MAXN * MAXN], V[MAXN * MAXN];
+    eye(I, n);
+    mm_plain(A, A, A2, n);
+    mm_plain(A, A2, A3, n);
+    const float* as[4] = {I, A, A2, A3};
+    for (int i = 0; i < 4; ++i) {
+        float c[4];
+        for (int j = 0; j < 4; ++j) c[j] = (float)B12[i][j];
+        lincomb(as, c, 4, Bs[i], n);
+    }
+    mm_plain(Bs[3], Bs[3], V, n); /* A6 */
+    add_inplace(Bs[2], V, n);
+    add_inplace(Bs[1], Bs[2], n);
+    mm_plain(Bs[1], Bs[2], V, n);
+    add_inplace(Bs[0], V, n);
+    memcpy(E, Bs[0], sizeof(float) * n * n);
+}
+
+static void T18(const float* A, float* E, int n) {
+    float I[MAXN * MAXN], A2[MAXN * MAXN], A3[MAXN * MAXN], A6[MAXN * MAXN];
+    float Bs[5][MAXN * MAXN], V[MAXN * MAXN];
+    eye(I, n);
+    mm_plain(A, A, A2, n);
+    mm_plain(A, A2, A3, n);
+    mm_plain(A3, A3, A6, n);
+    const float* as[5] = {I, A, A2, A3, A6};
+    for (int i = 0; i < 5; ++i) {
+        float c[5];
+        for (int j = 0; j < 5; ++j) c[j] = (float)B18[i][j];
+        lincomb(as, c, 5, Bs[i], n);
+    }
+    mm_plain(Bs[0], Bs[4], V, n); /* A9 */
+    add_inplace(Bs[3], V, n);
+    add_inplace(Bs[2], Bs[3], n);
+    mm_plain(Bs[2], Bs[3], V, n);
+    add_inplace(Bs[1], V, n);
+    memcpy(E, Bs[1], sizeof(float) * n * n);
+}
+
+static const float THETA[6] = {1.192092800768788e-07f, 5.978858893805233e-04f, 5.116619363445086e-02f,
+                               5.800524627688768e-01f, 1.461661507209034e+00f, 3.010066362817634e+00f};
+
+static float one_norm(const float* A, int n) {
+    float best = 0.0f;
+    for (int j = 0; j < n; ++j) {
+        float s = 0.0f;
+        for (int i = 0; i < n; ++i) s = s + fabsf(A[i * n + j]);
+        if (j == 0 || s > best) best = s;
+    }
+    return best;
+}
+
+static void T18_scale_square(const float* A, float* E, int n, float norm) {
+    float q = norm / THETA[5];
+    float l = ceilf(log2f(q));
+    long s = l > 0.0f ? (long)l : 0;
+    float As[MAXN * MAXN] = {0};
+    float scale = ldexpf(1.0f, (int)-s);
+    for (int e = 0; e < n * n; ++e) As[e] = A[e] * scale;
+    T18(As, E, n);
+    for (long p = 0; p < s; ++p) mm_plain(E, E, E, n);
+}
+
+/* torch.linalg.matrix_exp of one n x n matrix, taking the path torch takes for a
+ * batch of `batch` matrices. */
+static void expm_one(const float* A, float* E, int n, int batch) {
+    float norm = one_norm(A, n);
+    if (batch > 1) {
+        T18_scale_square(A, E, n, norm);
+        return;
+    }
+    if (isnan(norm)) {
+        for (int e = 0; e < n * n; ++e) E[e] = NAN;
+        return;
+    }
+    if (norm >= THETA[4]) {
+        T18_scale_square(A, E, n, norm);
+    } else if (norm <= THETA[0]) {
+        T1(A, E, n);
+    } else if (norm <= THETA[1]) {
+        T2(A, E, n);
+    } else if (norm <= THETA[2]) {
+        T4(A, E, n);
+    } else if (norm <= THETA[3]) {
+        T8(A, E, n);
+    } else {
+        T12(A, E, n);
+    }
+}
+
+void oracle_expm(const float* A, float* E, int n, int batch) {
+    for (int b = 0; b < batch; ++b) expm_one(A + (size_t)b * n * n, E + (size_t)b * n * n, n, batch);
+}
+
+/* warp.py:101-104: A = [[h5,h3,h1],[h4,-h5-h6,h2],[h7,h8,h6]] (1-based h) */
+static void sl3_generator(const float* h, float* A) {
+    A[0] = h[4];
+    A[1] = h[2];
+    A[2] = h[0];
+    A[3] = h[3];
+    A[4] = (-h[4]) - h[5];
+    A[5] = h[1];
+    A[6] = h[6];
+    A[7] = h[7];
+    A[8] = h[5];
+}
+
+void oracle_sl3_to_SL3(const float* h, float* H, int B) {
+    for (int b = 0; b < B; ++b) {
+        float A[9];
+        sl3_generator(h + 8 * b, A);
+        expm_one(A, H + 9 * b, 3, B);
+    }
+}
+
+/* d h from d H: torch's matrix_exp backward (exp of the 6x6 block matrix
+ * [[A^T, G],[0, A^T]], upper-right 3x3), then the generator's adjoint. */
+void oracle_sl3_to_SL3_backward(const float* h, const float* dH, float* dh, int B) {
+    for (int b = 0; b < B; ++b) {
+        float A[9], M[36], E[36], G[9];
+        sl3_generator(h + 8 * b, A);
+        memset(M, 0, sizeof(M));
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                M[i * 6 + j] = A[j * 3 + i];
+                M[(i + 3) * 6 + (j + 3)] = A[j * 3 + i];
+                M[i * 6 + (j + 3)] = dH[9 * b + i * 3 + j];
+            }
+        expm_one(M, E, 6, B);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) G[i * 3 + j] = E[i * 6 + (j + 3)];
+        float* d = dh + 8 * b;
+        d[0] = G[2];
+        d[1] = G[5];
+        d[2] = G[1];
+        d[3] = G[3];
+        d[4] = G[0] + (-G[4]);
+        d[5] = G[8] + (-G[4]);
+        d[6] = G[6];
+        d[7] = G[7];
+    }
+}
+
+/* ------------------------------------------------------------- grid and warp */
+
+/* warp.py:38-43 / 55-59: ((i + 0.5) / max * 2 - 1) * norm, fp32, true division. */
+static float grid_coord(int i, int maxdim, float norm) {
+    float t = (float)i + 0.5f;
+    t = t / (float)maxdim;
+    t = t * 2.0f;
+    t = t - 1.0f;
+    return t * norm;
+}
+
+/* Crop (crop=1) or full-canvas (crop=0) pixel grid, row-major p = r*w + c,
+ * one copy (the reference repeats it B times). xy: [h*w][2]. */
+void oracle_pixel_grid(int H, int W, int ph, int pw, int crop, float* xy) {
+    int mx = H > W ? H : W;
+    float norm_h = (float)((double)H / (double)mx);
+    float norm_w = (float)((double)W / (double)mx);
+    int y0 = 0, x0 = 0, h = H, w = W;
+    if (crop) {
+        y0 = H / 2 - ph / 2;
+        x0 = W / 2 - pw / 2;
+        h = (H / 2 + ph / 2) - y0;
+        w = (W / 2 + pw / 2) - x0;
+    }
+    for (int r = 0; r < h; ++r) {
+        float y = grid_coord(y0 + r, H, norm_h);
+        for (int c = 0; c < w; ++c) {
+            xy[2 * ((size_t)r * w + c) + 0] = grid_coord(x0 + c, W, norm_w);
+            xy[2 * ((size_t)r * w + c) + 1] = y;
+        }
+    }
+}
+
+/* warp.py:74-78 for one point: X = H [x y 1]^T as torch-CPU's bmm computes it
+ * (acc = x*H0; acc = fma(y, H1, acc); acc = acc + H2), then X[:2]/(X[2]+1e-8). */
+static void warp_point(const float* Hm, float x, float y, float* u, float* v, float* X) {
+    for (int r = 0; r < 3; ++r) {
+        float acc = x * Hm[3 * r + 0];
+        acc = fmaf(y, Hm[3 * r + 1], acc);
+        acc = acc + Hm[3 * r + 2];
+        X[r] = acc;
+    }
+    float d = X[2] + 1e-8f;
+    *u = X[0] / d;
+    *v = X[1] / d;
+}
+
+/* xy: [B][n][2] input points; Hm: [B][9]; uv: [B][n][2] output. */
+void oracle_warp_points(const float* xy, const float* Hm, float* uv, int B, int n) {
+    for (int b = 0; b < B; ++b)
+        for (int i = 0; i < n; ++i) {
+            float X[3];
+            const float* p = xy + 2 * ((size_t)b * n + i);
+            float* o = uv + 2 * ((size_t)b * n + i);
+            warp_point(Hm + 9 * b, p[0], p[1], &o[0], &o[1], X);
+        }
+}
+
+/* ----------------------------------------------------------------- posenc */
+
+/* c2f band weights, model/planar.py:462-467. progress, start, end as the
+ * reference holds them (progress fp32 Parameter; start/end python numbers). */
+void oracle_c2f_weights(float progress, double start, double end, int L, float* w) {
+    const float pi_f = (float)3.141592653589793;
+    float a = (progress - (float)start);
+    a = a / (float)(end - start);
+    a = a * (float)L;
+    for (int k = 0; k < L; ++k) {
+        float t = a - (float)k;
+        t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+        t = t * pi_f;
+        t = cosf(t);
+        w[k] = (1.0f - t) / 2.0f;
+    }
+}
+
+/* model/planar.py:429-434, 451-471: feat = [u, v, sin(f_k u), cos(f_k u), sin(f_k v),
+ * cos(f_k v)] (each block over k < L, multiplied by w_k when w != NULL),
+ * f_k = 2^k * pi_f32.  coord: [n][2], feat: [n][2+4L]. */
+void oracle_posenc(const float* coord, int n, int L, const float* w, float* feat) {
+    const float pi_f = (float)3.141592653589793;
+    int D = 2 + 4 * L;
+    for (int i = 0; i < n; ++i) {
+        float* f = feat + (size_t)i * D;
+        f[0] = coord[2 * i + 0];
+        f[1] = coord[2 * i + 1];
+        for (int c = 0; c < 2; ++c) {
+            float x = coord[2 * i + c];
+            for (int k = 0; k < L; ++k) {
+                float freq = ldexpf(1.0f, k) * pi_f;
+                float s = x * freq;
+                float sv = sinf(s), cv = cosf(s);
+                if (w) {
+                    sv = sv * w[k];
+                    cv = cv * w[k];
+                }
+                f[2 + c * 2 * L + k] = sv;
+                f[2 + c * 2 * L + L + k] = cv;
+            }
+        }
+    }
+}
+
+/* Adjoint of posenc + warp for one point: given d feat (dF[2+4L]), the point
+ * (x, y), H and the c2f weights, returns d(u,v) and accumulates dH[9] in double. */
+void oracle_prologue_backward(const float* xy, const float* Hm, const float* dfeat, int n, int L,
+                              const float* w, double* dH, float* duv) {
+    const float pi_f = (float)3.141592653589793;
+    int D = 2 + 4 * L;
+    for (int i = 0; i < n; ++i) {
+        float X[3], uv[2];
+        warp_point(Hm, xy[2 * i], xy[2 * i + 1], &uv[0], &uv[1], X);
+        const float* dF = dfeat + (size_t)i * D;
+        double g[2];
+        for (int c = 0; c < 2; ++c) {
+            double acc = dF[c];
+            for (int k = 0; k < L; ++k) {
+                float freq = ldexpf(1.0f, k) * pi_f;
+                float s = uv[c] * freq;
+                double wk = w ? w[k] : 1.0;
+                double ds = dF[2 + c * 2 * L + k] * wk, dc = dF[2 + c * 2 * L + L + k] * wk;
+                acc += (ds * cos((double)s) - dc * sin((double)s)) * (double)freq;
+            }
+            g[c] = acc;
+        }
+        if (duv) {
+            duv[2 * i] = (float)g[0];
+            duv[2 * i + 1] = (float)g[1];
+        }
+        if (dH) {
+            double d = (double)X[2] + (double)1e-8f;
+            double dX0 = g[0] / d, dX1 = g[1] / d;
+            double dX2 = -(g[0] * X[0] + g[1] * X[1]) / (d * d);
+            double p[3] = {xy[2 * i], xy[2 * i + 1], 1.0};
+            for (int c = 0; c < 3; ++c) {
+                dH[0 * 3 + c] += dX0 * p[c];
+                dH[1 * 3 + c] += dX1 * p[c];
+                dH[2 * 3 + c] += dX2 * p[c];
+            }
+        }
+    }
+}

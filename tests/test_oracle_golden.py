@@ -1,0 +1,160 @@
+"""The CPU oracle (oracle/) against golden vectors produced by the reference itself
+(tests/golden/make_golden.py).  CPU only: this pins the checker before it is used
+to judge the HIP path."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+
+def test_lie_exp_bitexact(golden):
+    g = golden("lie")
+    for tag in ("b64", "big"):
+        H = oracle.sl3_to_SL3(g[f"h_{tag}"])
+        assert np.array_equal(H, g[f"H_{tag}"]), tag
+    # torch takes the degree-selection path for a batch of exactly one
+    for i, h in enumerate(g["h_b1"]):
+        assert np.array_equal(oracle.sl3_to_SL3(h[None])[0], g["H_b1"][i]), i
+
+
+def test_lie_exp_backward_bitexact(golden):
+    g = golden("lie")
+    for tag in ("b5", "b1"):
+        dh = oracle.sl3_to_SL3_backward(g[f"bwd_h_{tag}"], g[f"bwd_dH_{tag}"])
+        assert np.array_equal(dh, g[f"bwd_dh_{tag}"]), tag
+
+
+@pytest.mark.parametrize("tag", ["c1", "c3"])
+def test_grid_and_warp_bitexact(golden, tag):
+    g = golden("prologue")
+    H, W, ph, pw, B = (int(x) for x in g[f"{tag}_geo"])
+    xy = oracle.pixel_grid(H, W, ph, pw, crop=True)
+    assert np.array_equal(xy[g[f"{tag}_idx"]], g[f"{tag}_xy"])
+    full = oracle.pixel_grid(H, W, ph, pw, crop=False)
+    assert np.array_equal(full[g[f"{tag}_full_idx"]], g[f"{tag}_full_xy"])
+    Hm = oracle.sl3_to_SL3(g[f"{tag}_h"])
+    assert np.array_equal(Hm, g[f"{tag}_H"])
+    uv = oracle.warp_points(np.broadcast_to(g[f"{tag}_xy"], (B,) + g[f"{tag}_xy"].shape).copy(), Hm)
+    assert np.array_equal(uv, g[f"{tag}_uv"])
+
+
+@pytest.mark.parametrize("tag", ["c1", "c3"])
+def test_posenc_c2f(golden, tag):
+    g = golden("prologue")
+    uv = g[f"{tag}_uv"][:, :256]
+    n = 0
+    for key in g.files:
+        if not key.startswith(f"{tag}_enc_"):
+            continue
+        _, _, Ls, mode, ps = key.split("_")
+        L, p = int(Ls[1:]), float(ps[1:])
+        w = oracle.c2f_weights(np.float32(p), [0, 0.4] if mode == "c2f" else None, L)
+        feat = oracle.posenc_features(uv, L, w)
+        ref = g[key]
+        assert np.array_equal(feat[..., :2], uv)
+        # sin/cos: glibc vs torch-CPU SLEEF may differ by 1 ulp; the arguments are exact
+        np.testing.assert_allclose(feat[..., 2:], ref, rtol=0, atol=2.5e-7, err_msg=key)
+        n += 1
+    assert n >= 6
+
+
+def test_c2f_known_answers():
+    # SURVEY.md §3.4 known answers (L=8, c2f [0, 0.4])
+    w = oracle.c2f_weights(np.float32(0.0), [0, 0.4], 8)
+    assert np.all(w == 0)
+    w = oracle.c2f_weights(np.float32(0.125), [0, 0.4], 8)
+    np.testing.assert_allclose(w, [1, 1, 0.5, 0, 0, 0, 0, 0], atol=1e-7)
+    w = oracle.c2f_weights(np.float32(0.39), [0, 0.4], 8)
+    np.testing.assert_allclose(w[-1], 0.904508, atol=1e-6)
+    assert np.all(oracle.c2f_weights(np.float32(0.4), [0, 0.4], 8) == 1)
+
+
+def _small_case(g, tag):
+    cfg = g[f"{tag}_cfg"]
+    H, W, ph, pw, B, L, c0, c1, max_iter, prog, use_edges = cfg
+    c2f = None if c0 < 0 else [c0, c1]
+    layers = g[f"{tag}_layers"]
+    params = [(g[f"{tag}_init_neural_image.mlp.{i}.weight"], g[f"{tag}_init_neural_image.mlp.{i}.bias"])
+              for i in range(len(layers) - 1)]
+    c = dict(H=int(H), W=int(W), patch_H=int(ph), patch_W=int(pw), L=int(L), c2f=c2f, max_iter=int(max_iter),
+             lr=1e-3, lr_warp=1e-3, fix_first=True, use_edges=bool(use_edges), alpha_initial=0.0, alpha_final=1.0)
+    st = oracle.PlanarStep(c, params, g[f"{tag}_warp0"], g[f"{tag}_rgb"], g[f"{tag}_mask"])
+    if prog >= 0:
+        st.progress = np.float32(prog)
+    return st, len(layers) - 1
+
+
+@pytest.mark.parametrize("tag", ["a", "b", "c", "d"])
+def test_small_step_vs_reference(golden, tag):
+    g = golden("step_small")
+    st, nl = _small_case(g, tag)
+    r = st.step()
+    np.testing.assert_allclose(r["rgb"].reshape(g[f"{tag}_rgb0"].shape), g[f"{tag}_rgb0"], atol=2e-6, rtol=0)
+    np.testing.assert_allclose(r["loss_rgb"], g[f"{tag}_loss"][0], rtol=2e-6)
+    for i in range(nl):
+        dW, db = r["grads"][i]
+        for name, got in (("weight", dW), ("bias", db)):
+            ref = g[f"{tag}_grad0_neural_image.mlp.{i}.{name}"]
+            scale = np.abs(ref).max() + 1e-12
+            assert np.abs(got - ref).max() / scale < 2e-5, (tag, i, name)
+    ref = g[f"{tag}_grad0_warp_param.weight"]
+    assert np.abs(r["dh"] - ref).max() / (np.abs(ref).max() + 1e-12) < 1e-4
+    # trajectory: 6 Adam steps with progress schedule and fix_first
+    traj = [st.warp.copy()]
+    losses = [r["loss_rgb"]]
+    for _ in range(5):
+        losses.append(st.step()["loss_rgb"])
+        traj.append(st.warp.copy())
+    np.testing.assert_allclose(np.array(losses), g[f"{tag}_loss"], rtol=1e-5)
+    np.testing.assert_allclose(np.stack(traj), g[f"{tag}_warp_traj"], atol=1e-5, rtol=0)
+    for i in range(nl):
+        np.testing.assert_allclose(st.params[i][0], g[f"{tag}_final_neural_image.mlp.{i}.weight"], atol=1e-5)
+
+
+def reference_init(layers_out, D_in, c2f, seed, B):
+    """RNG-ordered init of Graph (model/planar.py:303-311, 410-427) via torch."""
+    torch.manual_seed(seed)
+    params = []
+    k_in = D_in
+    for li, k_out in enumerate(layers_out):
+        lin = torch.nn.Linear(k_in, k_out)
+        if c2f is not None and li == 0:
+            scale = np.sqrt(D_in / 2.)
+            lin.weight.data *= scale
+            lin.bias.data *= scale
+        params.append((lin.weight.detach().numpy().copy(), lin.bias.detach().numpy().copy()))
+        k_in = k_out
+    torch.nn.Embedding(B, 8)
+    return params
+
+
+def test_c1_init_and_first_steps(golden):
+    """Real C1 (cat_batch3, seed 3, c2f [0,0.4], L=8): init checksums, the it=1
+    loss (0.050604186952114105 in the reference) and a 10-step trajectory."""
+    g = golden("step_c1")
+    imgs = golden("cat_batch3_c1")
+    rgb = imgs["rgb"].astype(np.float32) / np.float32(255)
+    mask = imgs["mask"].astype(np.float32)
+    assert np.isclose(rgb.astype(np.float64).sum(), g["rgb_checks"][0], rtol=1e-12)
+    assert mask.sum() == g["mask_sum"] == 183416
+    params = reference_init([256, 256, 256, 256, 3], 34, [0, 0.4], 3, 5)
+    for i, (W, b) in enumerate(params):
+        np.testing.assert_allclose(W.astype(np.float64).sum(), g[f"init_checks_neural_image.mlp.{i}.weight"][0], rtol=1e-9)
+        assert W.ravel()[0] == np.float32(g[f"init_checks_neural_image.mlp.{i}.weight"][3])
+    cfg = dict(H=360, W=480, patch_H=180, patch_W=240, L=8, c2f=[0, 0.4], max_iter=3000, lr=1e-3, lr_warp=1e-3,
+               fix_first=True, use_edges=True, alpha_initial=0.0, alpha_final=1.0)
+    st = oracle.PlanarStep(cfg, params, np.zeros((5, 8), np.float32), rgb, mask)
+    r = st.step()
+    np.testing.assert_allclose(r["loss_rgb"], 0.050604186952114105, rtol=1e-6)
+    np.testing.assert_allclose(r["rgb"][g["rgb0_idx"]], g["rgb0"], atol=2e-6)
+    for i in range(5):
+        ref = g[f"grad0_checks_neural_image.mlp.{i}.weight"]
+        got = r["grads"][i][0].astype(np.float64)
+        np.testing.assert_allclose([np.abs(got).sum(), (got * got).sum()], ref[1:3], rtol=1e-4)
+    np.testing.assert_allclose(r["dh"], g["grad0_warp"], atol=1e-4 * np.abs(g["grad0_warp"]).max())
+    losses = [r["loss_rgb"]]
+    for _ in range(9):
+        losses.append(st.step()["loss_rgb"])
+    np.testing.assert_allclose(losses, g["loss"], rtol=1e-5)
+    np.testing.assert_allclose(st.warp, g["warp_traj"][-1], atol=1e-6)
