@@ -1,0 +1,255 @@
+"""Throughput of the planar bundle-adjustment training step on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c1|c5] [--precision bf16|fp32]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one full Model.train_iteration of the product (model/planar.py): fused
+grid->warp->posenc->MLP forward, masked MSE, backward (dgrad chain, warp adjoint, weight
+gradients), the RCCL all-reduce of the MLP gradient (N > 1), Adam, progress update, fix_first.
+Workload (BASELINE.json configs[2]): per GPU 64 patches of 256x256 pixels cropped
+from a 512x512 canvas, L=16 posenc, MLP 66-256-256-256-256-3, bf16 MFMA, c2f [0,0.4] at
+progress 0.2.  Synthetic targets (smooth procedural RGB, seed 0), Bernoulli(0.85) masks (seed 1),
+warps ~ N(0, 0.01^2) (seed 2, patch 0 fixed).  Weak scaling: 64 patches per GPU at every N.
+
+Prints one JSON line (rank 0).  `value` = pixels processed by all ranks per second.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "masking-bundle-adjusting-neural-radiance-fields_amd")
+sys.path.insert(0, PKG)
+
+METRIC = "warped+encoded+MLP pixels/s/GPU; final PSNR vs ref (seed=3)"
+PEAK_BF16 = 2.5e15   # dense bf16 MFMA, MI355X_MICROARCH.md
+PEAK_FP32 = 157.3e12  # fp32 MFMA = vector rate
+PEAK_HBM = 8.0e12
+
+CONFIGS = {
+    # name: (canvas, crop, patches per GPU, L, hidden layers)
+    "c3": (512, 256, 64, 16, [256, 256, 256, 256]),
+    "c1": (None, None, 5, 8, [256, 256, 256, 256]),
+    "c5": (512, 256, 128, 16, [512] * 8),
+}
+
+
+def flops_per_px(dims):
+    """Algorithmic FLOPs of one pixel through a training step: 6 * sum k_in*k_out (fwd 2, dgrad 2,
+    wgrad 2 per MAC)."""
+    return 6 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+
+
+def make_opt(cfg, precision, B_total):
+    import options
+    from util import EasyDict as edict
+    canvas, crop, _, L, hidden = CONFIGS[cfg]
+    opt = options.load_options("options/planar.yaml")
+    over = {"model": "planar", "yaml": "planar", "seed": 3, "barf_c2f": [0, 0.4], "batch_size": B_total,
+            "precision": precision, "use_edges": False, "max_iter": 3000,
+            "arch": {"layers": [None] + hidden + [3], "skip": [], "posenc": {"L_2D": L}}}
+    if canvas:
+        over.update(H=canvas, W=canvas, patch_H=crop, patch_W=crop)
+    opt = options.override_options(opt, edict(over))
+    opt.output_path = os.path.join(ROOT, "output", "bench")
+    return opt
+
+
+def synthetic_inputs(B_total, h, w, device):
+    g0 = torch.Generator().manual_seed(0)
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, h), torch.linspace(0, 1, w), indexing="ij")
+    phase = torch.rand(B_total, 3, 1, 1, generator=g0) * 6.28
+    freq = 1 + 3 * torch.rand(B_total, 3, 2, generator=g0)
+    rgb = 0.5 + 0.4 * torch.sin(2 * np.pi * (freq[..., 0, None, None] * xx + freq[..., 1, None, None] * yy) + phase)
+    g1 = torch.Generator().manual_seed(1)
+    mask = (torch.rand(B_total, 1, h, w, generator=g1) < 0.85).float()
+    g2 = torch.Generator().manual_seed(2)
+    warp = torch.randn(B_total, 8, generator=g2) * 0.01
+    warp[0] = 0
+    return rgb.to(device), mask.to(device), warp.to(device)
+
+
+def cpu_baseline(cfg, sample_patches):
+    """The CPU oracle (oracle/, numpy + C) on a bounded sample of the same workload: one training
+    step over `sample_patches` patches, 1 warm-up + timed steps for ~10-30 s.  Pixels/s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        cores = os.cpu_count()
+    canvas, crop, _, L, hidden = CONFIGS[cfg]
+    if canvas is None:
+        canvas_h, canvas_w, ch, cw = 360, 480, 180, 240
+    else:
+        canvas_h = canvas_w = canvas
+        ch = cw = crop
+    rng = np.random.default_rng(0)
+    dims = [2 + 4 * L] + hidden + [3]
+    params = []
+    for a, b in zip(dims[:-1], dims[1:]):
+        bound = 1 / np.sqrt(a)
+        params.append((rng.uniform(-bound, bound, (b, a)).astype(np.float32),
+                       rng.uniform(-bound, bound, b).astype(np.float32)))
+    rgb = rng.random((sample_patches, 3, ch, cw)).astype(np.float32)
+    mask = (rng.random((sample_patches, 1, ch, cw)) < 0.85).astype(np.float32)
+    warp = (rng.standard_normal((sample_patches, 8)) * 0.01).astype(np.float32)
+    c = dict(H=canvas_h, W=canvas_w, patch_H=ch, patch_W=cw, L=L, c2f=[0, 0.4], max_iter=3000, lr=1e-3,
+             lr_warp=1e-3, fix_first=True, use_edges=False, alpha_initial=0.0, alpha_final=1.0)
+    st = oracle.PlanarStep(c, params, warp, rgb, mask)
+    st.progress = np.float32(0.2)
+    st.step()  # warm-up
+    times = []
+    t_end = time.time() + 20.0
+    while len(times) < 2 or (time.time() < t_end and len(times) < 8):
+        t0 = time.time()
+        st.step()
+        times.append(time.time() - t0)
+    px = sample_patches * ch * cw
+    return {"value": px / float(np.mean(times)), "unit": "pixels/s", "cores": int(cores), "kind": "port",
+            "sample": f"{sample_patches} patches x {ch}x{cw} px, {len(times)} timed oracle steps "
+                      f"(numpy fp32 sgemm + C prologue), mean {np.mean(times):.2f} s/step"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=list(CONFIGS))
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-patches", type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+
+    import marf_hip
+    from model import planar
+    from util import EasyDict as edict
+
+    canvas, crop, per_gpu, L, hidden = CONFIGS[args.config]
+    B_total = per_gpu * world
+    opt = make_opt(args.config, args.precision, B_total)
+    opt.device = str(dev)
+    h, w = opt.patch_H, opt.patch_W
+    torch.manual_seed(opt.seed)
+    m = planar.Model(opt)
+    rgb, mask, warp = synthetic_inputs(B_total, h, w, dev)
+    m.images = edict(rgb=rgb, masks=mask, masks_eroded=mask, edges=None, gt_hom=None, gt=None)
+    m.build_networks()
+    m.graph.warp_param.weight.data.copy_(warp)
+    m.graph.neural_image.progress.data.fill_(0.2)
+    m.setup_optimizer()
+    graph = m.graph
+    graph.need_edges = False
+    var = edict(idx=torch.arange(B_total), images=m.images)
+    b0, b1 = graph.shard if graph.shard else (0, B_total)
+    px_local = (b1 - b0) * h * w
+
+    def step():
+        m.optim.zero_grad()
+        v = graph.forward(var, mode="train")
+        loss = graph.compute_loss(v, mode="train")
+        total = 0.
+        for key in loss:  # Model.summarize_loss without its host-side NaN asserts
+            if opt.loss_weight[key] is not None:
+                total = total + 10 ** float(opt.loss_weight[key]) * loss[key]
+        total.backward()
+        m.all_reduce_grads()
+        m.optim.step()
+        graph.neural_image.progress.data.fill_(0.2)  # keep c2f partially on
+        graph.warp_param.weight.data[0] = 0
+        return loss
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        loss = step()
+    barrier()
+    marf_hip.profile_reset()
+    marf_hip.profile_enable(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    marf_hip.profile_enable(False)
+    prof = marf_hip.profile_read()
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t)
+    loss_v = float(loss.rgb)
+    assert np.isfinite(loss_v), "loss is not finite"
+
+    # ---- roofline of the dominant kernel (HIP-event durations measured above, same stream)
+    dims = [2 + 4 * L] + hidden + [3]
+    Kp0 = (dims[0] + 31) // 32 * 32
+    S = (b1 - b0) * ((h * w + 127) // 128 * 128)
+    layer_flops = [2 * a * b for a, b in zip(dims[:-1], dims[1:])]
+    kflops = {
+        "mlp_fwd": S * sum(layer_flops),
+        "mlp_bwd_dgrad": S * sum(layer_flops),
+        "wgrad_hidden": S * 2 * hidden[0] * hidden[0],
+        "wgrad_l0": S * 2 * dims[0] * dims[1],
+    }
+    per_kernel = {k: {"avg_ms": v[0] / v[1], "launches_per_step": v[1] / args.steps} for k, v in prof.items()}
+    step_kernel_ms = sum(v[0] for v in prof.values()) / args.steps
+    dom = max(prof.items(), key=lambda kv: kv[1][0])[0] if prof else None
+    peak = PEAK_BF16 if args.precision == "bf16" else PEAK_FP32
+    roof = None
+    if dom in kflops:
+        avg_s = prof[dom][0] / prof[dom][1] / 1e3
+        ach = kflops[dom] / avg_s
+        roof = {"kernel": dom, "bound": "mfma", "achieved": ach / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
+                "frac": ach / peak, "traffic": None,
+                "algorithmic_flops_per_launch": kflops[dom], "avg_launch_ms": avg_s * 1e3}
+    ms = elapsed / args.steps * 1e3
+    value = world * px_local / (elapsed / args.steps)
+    F = flops_per_px(dims)
+    out = {
+        "metric": METRIC, "value": value, "unit": "pixels/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+        "config": {"workload": f"{args.config}: {per_gpu} patches x {h}x{w} px per GPU, L={L}, MLP "
+                               f"{'-'.join(map(str, dims))}, {args.precision}, c2f [0,0.4] at progress 0.2",
+                   "patches_per_gpu": per_gpu, "pixels_per_step_per_gpu": px_local,
+                   "pixels_per_s_per_gpu": value / world, "parallelism": f"dp{world} (patches)",
+                   "algorithmic_flops_per_px": F,
+                   "step_tflops_per_gpu": value / world * F / 1e12,
+                   "step_frac_of_peak": value / world * F / peak,
+                   "loss_rgb_last": loss_v},
+        "roofline": roof,
+        "kernels": per_kernel,
+        "kernel_ms_per_step": step_kernel_ms,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_patches)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,128 @@
+/*
+ * marf.h -- C ABI of libmarf.so, the MI355X (gfx950) implementation of the planar
+ * bundle-adjustment render loop of thomasjaron/masking-bundle-adjusting-neural-radiance-fields
+ * (model/planar.py + warp.py).
+ *
+ * The reference has no FFI: its boundary is the Python module API.  Each entry
+ * point below replaces the reference interface named in its comment; the Python host package
+ * (masking-bundle-adjusting-neural-radiance-fields_amd/marf_hip.py) binds them with ctypes and
+ * keeps the reference's module / autograd contract on top.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Every pointer argument named d_* / device is HIP device
+ *     memory owned by the caller (PyTorch's allocator); the library borrows it for the call.
+ *   - `stream` is a hipStream_t passed as void*; every call is asynchronous on it, no implicit
+ *     device synchronisation, no allocation on the step path.
+ *   - Every function returns 0 on success or a negative MARF_ERR_* code; marf_last_error()
+ *     returns a thread-local message for the last failure.
+ *   - float32 everywhere in the interface; dtype selects the internal MLP arithmetic
+ *     (MARF_FP32 = exact fp32 MFMA, MARF_BF16 = bf16 MFMA with fp32 accumulation).
+ */
+#ifndef MARF_H
+#define MARF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MARF_OK 0
+#define MARF_ERR_INVALID -1   /* bad argument / shape (reference: AssertionError) */
+#define MARF_ERR_HIP -2       /* HIP runtime error */
+#define MARF_ERR_UNSUPPORTED -3
+
+#define MARF_FP32 0
+#define MARF_BF16 1
+
+#define MARF_GEO_GRID 0   /* pixels of the centre crop, warped by a per-patch homography */
+#define MARF_GEO_COORDS 1 /* explicit [n][2] coordinates (one point set) */
+
+typedef struct marf_net marf_net; /* opaque: MLP shape + padding plan */
+
+typedef struct {
+    int mode;             /* MARF_GEO_GRID or MARF_GEO_COORDS */
+    int B;                /* patches (GRID) ; must be 1 for COORDS */
+    int Np;               /* GRID: patch_H*patch_W (computed); COORDS: number of points */
+    int H, W;             /* canvas (opt.H, opt.W) */
+    int patch_H, patch_W; /* crop (opt.patch_H, opt.patch_W) */
+    const float* d_H;     /* GRID: [B][3][3] homographies (from marf_sl3_to_SL3) */
+    const float* d_coords;/* COORDS: [Np][2] */
+} marf_geometry;
+
+typedef struct {
+    const float* d_progress; /* fp32 scalar on device (NeuralImageFunction.progress) */
+    double start, end;       /* opt.barf_c2f */
+    int on;                  /* 0: barf_c2f is None (no band weighting) */
+} marf_c2f;
+
+const char* marf_last_error(void);
+int marf_version(void);
+
+/* ---- Lie group (warp.py:95-106 Lie.sl3_to_SL3; torch.linalg.matrix_exp semantics).
+ * lie_batch: the batch size torch would see (selects torch's path; pass B unless sharded). */
+int marf_sl3_to_SL3(const float* d_h, float* d_H, int B, int lie_batch, void* stream);
+int marf_sl3_to_SL3_backward(const float* d_h, const float* d_dH, float* d_dh, int B, int lie_batch, void* stream);
+
+/* ---- Warp (warp.py:33-68 get_normalized_pixel_grid, one copy [n][2]; warp.py:70-81 warp_grid) */
+int marf_pixel_grid(int H, int W, int patch_H, int patch_W, int crop, float* d_xy, void* stream);
+int marf_warp_points(const float* d_xy, const float* d_H, float* d_uv, int B, int n, int xy_shared, void* stream);
+
+/* ---- Positional encoding + c2f (model/planar.py:451-471): [n][2] -> [n][4L] */
+int marf_posenc(const float* d_coord, long long n, int L, const marf_c2f* c2f, float* d_enc, void* stream);
+
+/* ---- Neural image MLP (model/planar.py:395-449, NeuralImageFunction)
+ * dims[0] = 2 + 4L (input), dims[n_layers] = 3, hidden dims arbitrary (padded internally).
+ * Flat fp32 parameter vector layout = NeuralImageFunction.mlp parameters in module order:
+ * W0 [dims1][dims0], b0 [dims1], W1, b1, ...  (nn.Linear layout). */
+int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** out);
+void marf_net_destroy(marf_net* net);
+long long marf_net_param_count(const marf_net* net);
+size_t marf_net_packed_bytes(const marf_net* net);
+/* fp32 master parameters -> MFMA operand layouts (call after every optimizer step). */
+int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, void* stream);
+
+/* Bytes of the activation cache the backward needs, and of the backward scratch. */
+size_t marf_saved_bytes(const marf_net* net, const marf_geometry* geo);
+size_t marf_workspace_bytes(const marf_net* net, const marf_geometry* geo);
+
+/* Forward (Graph.forward model/planar.py:329-335 for GRID: grid -> warp -> posenc -> MLP;
+ * NeuralImageFunction.forward :429 for COORDS).  rgb: [B][Np][3].  d_saved NULL = inference. */
+int marf_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
+                 float* d_rgb, void* d_saved, void* stream);
+
+/* Backward of marf_forward given d loss / d rgb.  Writes (overwrites) d_params (flat, fp32),
+ * and d_h [B][8] (GRID, needs d_h_params = the sl(3) warp parameters) or d_coords [Np][2]
+ * (COORDS).  Any output pointer may be NULL. */
+int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
+                  const float* d_h_params, int lie_batch, const float* d_rgb_out, const float* d_drgb,
+                  const void* d_saved, void* d_workspace, float* d_dparams, float* d_dh, float* d_dcoords,
+                  void* stream);
+
+/* ---- Masked MSE (Graph.mse_loss, model/planar.py:382-391).  pred [B][Np][3] (MLP layout),
+ * gt [B][3][Np], mask [B][1][Np] or NULL (plain mean).  d_out[3]: loss, denominator used,
+ * local 3*sum(mask).  d_denom_override: optional device scalar (global denominator of a patch
+ * shard).  d_ws: marf_mse_workspace_bytes(). */
+size_t marf_mse_workspace_bytes(void);
+int marf_masked_mse(const float* d_pred, const float* d_gt, const float* d_mask, int B, int Np,
+                    const float* d_denom_override, float* d_out, void* d_ws, void* stream);
+int marf_masked_mse_backward(const float* d_pred, const float* d_gt, const float* d_mask, int B, int Np,
+                             const float* d_denom, const float* d_gout, float* d_dpred, void* stream);
+
+/* ---- Adam (torch.optim.Adam, model/planar.py:98-99): one parameter segment, step >= 1.
+ * d_grad_scale: optional device scalar multiplying the gradient (NULL = 1). */
+int marf_adam_step(float* d_p, const float* d_g, float* d_m, float* d_v, long long n, double lr, double beta1,
+                   double beta2, double eps, long long step, const float* d_grad_scale, void* stream);
+
+/* ---- Profiling: HIP events recorded around each kernel on its launch stream (off by default).
+ * marf_profile_read drains the recorded pairs (synchronising on them) and returns, per kernel
+ * name, the summed duration (ms) and launch count; names is a [cap][name_len] char array. */
+int marf_profile_enable(int on);
+int marf_profile_reset(void);
+int marf_profile_read(char* names, int name_len, double* total_ms, long long* count, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MARF_H */

@@ -1,0 +1,46 @@
+"""Build libmarf.so (all HIP sources, gfx950 only) in-tree: lib/libmarf.so.
+
+    python build_lib.py [--force]
+
+The library is rebuilt when any source under csrc/ or include/ is newer than it.
+"""
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "lib", "libmarf.so")
+SOURCES = ["marf_lie.hip", "marf_mlp.hip", "marf_wgrad.hip", "marf_misc.hip", "marf_abi.hip", "marf_prof.hip"]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+         # exact fp32 operation order for the bit-exact prologue (no implicit FMA contraction)
+         "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = glob.glob(os.path.join(HERE, "csrc", "*")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=True):
+    if not force and not _stale():
+        return LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc] + FLAGS + [os.path.join(HERE, "csrc", s) for s in SOURCES] + ["-o", tmp]
+    if verbose:
+        print("[marf] building", LIB, flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

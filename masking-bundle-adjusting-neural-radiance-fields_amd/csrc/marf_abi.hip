@@ -1,0 +1,500 @@
+// marf_abi.hip -- extern "C" entry points of libmarf.so (declared in include/marf.h).
+// Host-side validation, buffer planning and kernel launches; no device allocation here: every
+// buffer is owned by the caller (PyTorch's caching allocator).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/marf.h"
+#include "marf_args.h"
+#include "marf_prof.h"
+
+using namespace marf;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+static int check_hip(hipError_t e, const char* what) {
+    if (e != hipSuccess) return fail(MARF_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    return MARF_OK;
+}
+
+#define HIPCHK(expr, what)                          \
+    do {                                            \
+        int _rc = check_hip((expr), (what));        \
+        if (_rc != MARF_OK) return _rc;             \
+    } while (0)
+
+static inline long long rup(long long x, long long m) { return (x + m - 1) / m * m; }
+
+struct marf_net {
+    int n_layers, L, D, dtype;
+    int dims[MARF_MAX_LAYERS + 1];
+    int Kp[MARF_MAX_LAYERS], Mp[MARF_MAX_LAYERS], Mt[MARF_MAX_LAYERS];
+    long long w_off[MARF_MAX_LAYERS], b_off[MARF_MAX_LAYERS], param_count;
+    long long wf_off[MARF_MAX_LAYERS], wt_off[MARF_MAX_LAYERS], bias_off[MARF_MAX_LAYERS];
+    size_t packed_bytes;
+    int TP, lda, Kmax;
+    size_t lds_fwd, lds_bwd;
+    int elem;  // bytes per stored element
+};
+
+extern "C" {
+
+const char* marf_last_error(void) { return g_err.c_str(); }
+int marf_version(void) { return 1; }
+
+// ------------------------------------------------------------------ Lie / warp / posenc
+
+int marf_sl3_to_SL3(const float* d_h, float* d_H, int B, int lie_batch, void* stream) {
+    if (B < 0 || (B > 0 && (!d_h || !d_H))) return fail(MARF_ERR_INVALID, "sl3_to_SL3: bad arguments");
+    MarfProfScope ps("lie_exp", (hipStream_t)stream);
+    HIPCHK(marf_launch_sl3(d_h, d_H, B, lie_batch > 0 ? lie_batch : B, (hipStream_t)stream), "sl3_to_SL3");
+    return MARF_OK;
+}
+
+int marf_sl3_to_SL3_backward(const float* d_h, const float* d_dH, float* d_dh, int B, int lie_batch, void* stream) {
+    if (B < 0 || (B > 0 && (!d_h || !d_dH || !d_dh))) return fail(MARF_ERR_INVALID, "sl3_to_SL3_backward: bad arguments");
+    HIPCHK(marf_launch_sl3_bwd(d_h, d_dH, d_dh, B, lie_batch > 0 ? lie_batch : B, (hipStream_t)stream),
+           "sl3_to_SL3_backward");
+    return MARF_OK;
+}
+
+static int make_geo(const marf_geometry* g, GeoDev& d, int TP_pad) {
+    if (!g) return fail(MARF_ERR_INVALID, "geometry is NULL");
+    memset(&d, 0, sizeof(d));
+    d.mode = g->mode;
+    if (g->mode == MARF_GEO_GRID) {
+        if (g->B <= 0 || g->H <= 0 || g->W <= 0 || g->patch_H <= 1 || g->patch_W <= 1 || g->patch_H > g->H ||
+            g->patch_W > g->W)
+            return fail(MARF_ERR_INVALID, "grid geometry: B=%d H=%d W=%d patch=%dx%d", g->B, g->H, g->W, g->patch_H,
+                        g->patch_W);
+        if (!g->d_H) return fail(MARF_ERR_INVALID, "grid geometry needs d_H");
+        // warp.py:14-19: crop window = centre +- half (integer division, as the reference)
+        int y0 = g->H / 2 - g->patch_H / 2, y1 = g->H / 2 + g->patch_H / 2;
+        int x0 = g->W / 2 - g->patch_W / 2, x1 = g->W / 2 + g->patch_W / 2;
+        d.B = g->B;
+        d.y0 = y0;
+        d.x0 = x0;
+        d.w = x1 - x0;
+        d.Np = (y1 - y0) * (x1 - x0);
+        d.H = g->H;
+        d.W = g->W;
+        int mx = std::max(g->H, g->W);
+        d.norm_h = (float)((double)g->H / (double)mx);
+        d.norm_w = (float)((double)g->W / (double)mx);
+        d.Hm = g->d_H;
+    } else if (g->mode == MARF_GEO_COORDS) {
+        if (g->B != 1 || g->Np <= 0 || !g->d_coords)
+            return fail(MARF_ERR_INVALID, "coords geometry: B must be 1, Np > 0, coords given");
+        d.B = 1;
+        d.Np = g->Np;
+        d.coords = g->d_coords;
+        d.w = 1;
+    } else {
+        return fail(MARF_ERR_INVALID, "unknown geometry mode %d", g->mode);
+    }
+    d.Np_pad = (int)rup(d.Np, TP_pad);
+    d.bmm_small = (d.mode == MARF_GEO_GRID && 9LL * d.Np < 400) ? 1 : 0;
+    return MARF_OK;
+}
+
+int marf_pixel_grid(int H, int W, int patch_H, int patch_W, int crop, float* d_xy, void* stream) {
+    if (H <= 0 || W <= 0 || !d_xy) return fail(MARF_ERR_INVALID, "pixel_grid: bad arguments");
+    GeoDev g;
+    memset(&g, 0, sizeof(g));
+    int mx = std::max(H, W);
+    g.H = H;
+    g.W = W;
+    g.norm_h = (float)((double)H / (double)mx);
+    g.norm_w = (float)((double)W / (double)mx);
+    int h = H;
+    if (crop) {
+        if (patch_H <= 0 || patch_W <= 0 || patch_H > H || patch_W > W)
+            return fail(MARF_ERR_INVALID, "pixel_grid: bad crop %dx%d", patch_H, patch_W);
+        g.y0 = H / 2 - patch_H / 2;
+        g.x0 = W / 2 - patch_W / 2;
+        h = (H / 2 + patch_H / 2) - g.y0;
+        g.w = (W / 2 + patch_W / 2) - g.x0;
+    } else {
+        g.w = W;
+    }
+    HIPCHK(marf_launch_pixel_grid(g, d_xy, h * g.w, (hipStream_t)stream), "pixel_grid");
+    return MARF_OK;
+}
+
+int marf_warp_points(const float* d_xy, const float* d_H, float* d_uv, int B, int n, int xy_shared, void* stream) {
+    if (B <= 0 || n < 0 || !d_xy || !d_H || !d_uv) return fail(MARF_ERR_INVALID, "warp_points: bad arguments");
+    if (n == 0) return MARF_OK;
+    HIPCHK(marf_launch_warp_points(d_xy, d_H, d_uv, B, n, xy_shared, (hipStream_t)stream), "warp_points");
+    return MARF_OK;
+}
+
+static C2fDev make_c2f(const marf_c2f* c) {
+    C2fDev d;
+    memset(&d, 0, sizeof(d));
+    if (c && c->on && c->d_progress) {
+        d.on = 1;
+        d.progress = c->d_progress;
+        d.start = (float)c->start;
+        d.span = (float)(c->end - c->start);
+    }
+    return d;
+}
+
+int marf_posenc(const float* d_coord, long long n, int L, const marf_c2f* c2f, float* d_enc, void* stream) {
+    if (n < 0 || L <= 0 || L > 32 || !d_coord || !d_enc) return fail(MARF_ERR_INVALID, "posenc: bad arguments");
+    if (n == 0) return MARF_OK;
+    C2fDev c = make_c2f(c2f);
+    HIPCHK(marf_launch_posenc(d_coord, n, L, c.progress, c.start, c.span, c.on, d_enc, (hipStream_t)stream), "posenc");
+    return MARF_OK;
+}
+
+// ------------------------------------------------------------------ network
+
+int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** out) {
+    if (!out || !dims) return fail(MARF_ERR_INVALID, "net_create: NULL argument");
+    *out = nullptr;
+    if (n_layers < 2 || n_layers > MARF_MAX_LAYERS)
+        return fail(MARF_ERR_UNSUPPORTED, "net_create: n_layers=%d (supported 2..%d)", n_layers, MARF_MAX_LAYERS);
+    if (dtype != MARF_FP32 && dtype != MARF_BF16) return fail(MARF_ERR_INVALID, "net_create: dtype %d", dtype);
+    if (L < 0 || L > 32) return fail(MARF_ERR_UNSUPPORTED, "net_create: L=%d (supported 0..32)", L);
+    int D = L > 0 ? 2 + 4 * L : 2;
+    if (dims[0] != D) return fail(MARF_ERR_INVALID, "net_create: dims[0]=%d but 2+4L=%d", dims[0], D);
+    if (dims[n_layers] != 3) return fail(MARF_ERR_INVALID, "net_create: output dim %d != 3", dims[n_layers]);
+    marf_net* n = new marf_net;
+    memset(n, 0, sizeof(*n));
+    n->n_layers = n_layers;
+    n->L = L;
+    n->D = D;
+    n->dtype = dtype;
+    n->elem = dtype == MARF_BF16 ? 2 : 4;
+    for (int i = 0; i <= n_layers; ++i) {
+        if (dims[i] <= 0) {
+            delete n;
+            return fail(MARF_ERR_INVALID, "net_create: dims[%d]=%d", i, dims[i]);
+        }
+        n->dims[i] = dims[i];
+    }
+    n->Kp[0] = (int)rup(D, 32);
+    int hmax = 0;
+    for (int l = 0; l < n_layers - 1; ++l) {
+        n->Mp[l] = (int)rup(dims[l + 1], 32);
+        n->Mt[l] = n->Mp[l];
+        n->Kp[l + 1] = n->Mp[l];
+        hmax = std::max(hmax, n->Mp[l]);
+    }
+    n->Mp[n_layers - 1] = 16;
+    n->Mt[n_layers - 1] = dtype == MARF_BF16 ? 16 : 4;
+    n->Kmax = 0;
+    for (int l = 0; l < n_layers; ++l) n->Kmax = std::max(n->Kmax, n->Kp[l]);
+    if (hmax > 512 || n->Kmax > 512) {
+        delete n;
+        return fail(MARF_ERR_UNSUPPORTED, "net_create: hidden width %d > 512", hmax);
+    }
+    n->TP = (dtype == MARF_BF16 && n->Kmax <= 256) ? 128 : 64;
+    n->lda = dtype == MARF_BF16 ? n->Kmax + 8 : n->Kmax + 1;
+    size_t act = (size_t)n->TP * n->lda * n->elem;
+    size_t df = (size_t)n->TP * (n->Kp[0] + 1) * 4;
+    n->lds_fwd = act;
+    n->lds_bwd = std::max(act, df);
+    if (n->lds_bwd > 160 * 1024) {
+        delete n;
+        return fail(MARF_ERR_UNSUPPORTED, "net_create: tile does not fit LDS");
+    }
+    long long off = 0;
+    size_t boff = 0;
+    for (int l = 0; l < n_layers; ++l) {
+        n->w_off[l] = off;
+        off += (long long)dims[l + 1] * dims[l];
+        n->b_off[l] = off;
+        off += dims[l + 1];
+        n->wf_off[l] = (long long)boff;
+        boff += rup((long long)n->Mp[l] * n->Kp[l] * n->elem, 256);
+        n->wt_off[l] = (long long)boff;
+        boff += rup((long long)n->Kp[l] * n->Mt[l] * n->elem, 256);
+        n->bias_off[l] = (long long)boff;
+        boff += rup((long long)n->Mp[l] * 4, 256);
+    }
+    n->param_count = off;
+    n->packed_bytes = boff;
+    *out = n;
+    return MARF_OK;
+}
+
+void marf_net_destroy(marf_net* net) { delete net; }
+long long marf_net_param_count(const marf_net* net) { return net ? net->param_count : -1; }
+size_t marf_net_packed_bytes(const marf_net* net) { return net ? net->packed_bytes : 0; }
+
+int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, void* stream) {
+    if (!net || !d_params || !d_packed) return fail(MARF_ERR_INVALID, "net_pack: NULL argument");
+    PackArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n_layers = net->n_layers;
+    long long mx = 0;
+    for (int l = 0; l < net->n_layers; ++l) {
+        PackLayer& p = a.ly[l];
+        p.M = net->dims[l + 1];
+        p.K = net->dims[l];
+        p.Mp = net->Mp[l];
+        p.Kp = net->Kp[l];
+        p.Mt = net->Mt[l];
+        p.w_off = net->w_off[l];
+        p.b_off = net->b_off[l];
+        p.wf_off = net->wf_off[l];
+        p.wt_off = net->wt_off[l];
+        p.bias_off = net->bias_off[l];
+        mx = std::max(mx, (long long)p.Mp * p.Kp + (long long)p.Kp * p.Mt + p.Mp);
+    }
+    MarfProfScope ps("pack_weights", (hipStream_t)stream);
+    HIPCHK(marf_launch_pack(net->dtype, d_params, (char*)d_packed, a, mx, (hipStream_t)stream), "net_pack");
+    return MARF_OK;
+}
+
+static void fill_netdev(const marf_net* n, const void* packed, NetDev& d) {
+    memset(&d, 0, sizeof(d));
+    d.n_layers = n->n_layers;
+    d.L = n->L;
+    d.D = n->D;
+    for (int l = 0; l < n->n_layers; ++l) {
+        d.Kp[l] = n->Kp[l];
+        d.Mp[l] = n->Mp[l];
+        d.Mt[l] = n->Mt[l];
+        d.Wf[l] = (const char*)packed + n->wf_off[l];
+        d.Wt[l] = (const char*)packed + n->wt_off[l];
+        d.bias[l] = (const float*)((const char*)packed + n->bias_off[l]);
+    }
+}
+
+// ------------------------------------------------------------------ buffer plans
+
+struct SavedPlan {
+    size_t feat[MARF_MAX_LAYERS], mask[MARF_MAX_LAYERS], total;
+};
+
+static void plan_saved(const marf_net* n, long long S, SavedPlan& p) {
+    size_t off = 0;
+    for (int l = 0; l < n->n_layers; ++l) {
+        p.feat[l] = off;
+        off += rup((long long)S * n->Kp[l] * n->elem, 256);
+    }
+    p.mask[0] = 0;
+    for (int l = 1; l < n->n_layers; ++l) {
+        p.mask[l] = off;
+        off += rup((long long)(n->Kp[l] / 32) * S * 4, 256);
+    }
+    p.total = off;
+}
+
+struct WsPlan {
+    size_t dz[MARF_MAX_LAYERS], glast, dH, part, bpart, total;
+    int chunk, n_chunks, n_tiles;
+};
+
+static void plan_ws(const marf_net* n, long long S, int n_tiles, WsPlan& p) {
+    size_t off = 0;
+    p.dz[0] = 0;
+    for (int l = 1; l < n->n_layers; ++l) {
+        p.dz[l] = off;
+        off += rup((long long)S * n->Kp[l] * n->elem, 256);
+    }
+    p.glast = off;
+    off += rup(S * 16, 256);
+    p.dH = off;
+    off += rup((long long)n_tiles * 9 * 4, 256);
+    long long chunk = rup((S + 255) / 256, 64);
+    if (chunk < 64) chunk = 64;
+    p.chunk = (int)chunk;
+    p.n_chunks = (int)((S + chunk - 1) / chunk);
+    p.n_tiles = n_tiles;
+    long long mxo = 0, mxm = 0;
+    for (int l = 0; l < n->n_layers - 1; ++l) {
+        mxo = std::max(mxo, (long long)n->Mp[l] * n->Kp[l]);
+        mxm = std::max(mxm, (long long)n->Mp[l]);
+    }
+    mxo = std::max(mxo, 3LL * n->Kp[n->n_layers - 1]);
+    p.part = off;
+    off += rup((long long)p.n_chunks * mxo * 4, 256);
+    p.bpart = off;
+    off += rup((long long)p.n_chunks * std::max(mxm, 3LL) * 4, 256);
+    p.total = off;
+}
+
+size_t marf_saved_bytes(const marf_net* net, const marf_geometry* geo) {
+    GeoDev g;
+    if (!net || make_geo(geo, g, MARF_TILE_PAD) != MARF_OK) return 0;
+    SavedPlan p;
+    plan_saved(net, (long long)g.B * g.Np_pad, p);
+    return p.total;
+}
+
+size_t marf_workspace_bytes(const marf_net* net, const marf_geometry* geo) {
+    GeoDev g;
+    if (!net || make_geo(geo, g, MARF_TILE_PAD) != MARF_OK) return 0;
+    long long S = (long long)g.B * g.Np_pad;
+    WsPlan p;
+    plan_ws(net, S, (int)(S / net->TP), p);
+    return p.total;
+}
+
+// ------------------------------------------------------------------ forward / backward
+
+int marf_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
+                 float* d_rgb, void* d_saved, void* stream) {
+    if (!net || !d_packed || !d_rgb) return fail(MARF_ERR_INVALID, "forward: NULL argument");
+    FwdArgs a;
+    memset(&a, 0, sizeof(a));
+    int rc = make_geo(geo, a.geo, MARF_TILE_PAD);
+    if (rc) return rc;
+    fill_netdev(net, d_packed, a.net);
+    a.c2f = make_c2f(c2f);
+    a.rgb = d_rgb;
+    a.S = (long long)a.geo.B * a.geo.Np_pad;
+    a.lda = net->lda;
+    if (d_saved) {
+        SavedPlan p;
+        plan_saved(net, a.S, p);
+        for (int l = 0; l < net->n_layers; ++l) a.feat[l] = (char*)d_saved + p.feat[l];
+        for (int l = 1; l < net->n_layers; ++l) a.mask[l] = (uint32_t*)((char*)d_saved + p.mask[l]);
+    }
+    int n_tiles = (int)(a.S / net->TP);
+    {
+        MarfProfScope ps("mlp_fwd", (hipStream_t)stream);
+        HIPCHK(marf_launch_mlp_fwd(a, net->dtype, net->TP, net->lds_fwd, n_tiles, (hipStream_t)stream), "forward");
+    }
+    return MARF_OK;
+}
+
+int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
+                  const float* d_h_params, int lie_batch, const float* d_rgb_out, const float* d_drgb,
+                  const void* d_saved, void* d_workspace, float* d_dparams, float* d_dh, float* d_dcoords,
+                  void* stream) {
+    if (!net || !d_packed || !d_rgb_out || !d_drgb || !d_saved || !d_workspace)
+        return fail(MARF_ERR_INVALID, "backward: NULL argument");
+    hipStream_t s = (hipStream_t)stream;
+    BwdArgs a;
+    memset(&a, 0, sizeof(a));
+    int rc = make_geo(geo, a.geo, MARF_TILE_PAD);
+    if (rc) return rc;
+    if (a.geo.mode == MARF_GEO_GRID && d_dh && !d_h_params)
+        return fail(MARF_ERR_INVALID, "backward: d_dh requested without the warp parameters");
+    fill_netdev(net, d_packed, a.net);
+    a.c2f = make_c2f(c2f);
+    a.rgb = d_rgb_out;
+    a.d_rgb = d_drgb;
+    a.S = (long long)a.geo.B * a.geo.Np_pad;
+    a.lda = net->lda;
+    const int n_tiles = (int)(a.S / net->TP);
+    SavedPlan sp;
+    plan_saved(net, a.S, sp);
+    WsPlan wp;
+    plan_ws(net, a.S, n_tiles, wp);
+    char* ws = (char*)d_workspace;
+    const char* sv = (const char*)d_saved;
+    for (int l = 1; l < net->n_layers; ++l) {
+        a.mask[l] = (const uint32_t*)(sv + sp.mask[l]);
+        a.dz[l] = ws + wp.dz[l];
+    }
+    a.glast = (float*)(ws + wp.glast);
+    a.dH_partial = (float*)(ws + wp.dH);
+    a.d_coords = d_dcoords;
+    if (a.geo.mode == MARF_GEO_COORDS && !d_dcoords) {
+        // d coords not wanted: route them to the partial buffer is not possible -> use glast tail
+        a.d_coords = nullptr;
+    }
+    {
+        MarfProfScope ps("mlp_bwd_dgrad", s);
+        HIPCHK(marf_launch_mlp_bwd(a, net->dtype, net->TP, net->lds_bwd, n_tiles, s), "backward dgrad");
+    }
+
+    if (d_dparams) {
+        float* part = (float*)(ws + wp.part);
+        float* bpart = (float*)(ws + wp.bpart);
+        const int nl = net->n_layers;
+        for (int l = 0; l < nl - 1; ++l) {
+            {
+                MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
+                HIPCHK(marf_launch_wgrad(net->dtype, ws + wp.dz[l + 1], net->Kp[l + 1], sv + sp.feat[l], net->Kp[l],
+                                         a.S, net->Mp[l], net->Kp[l], wp.chunk, wp.n_chunks, part, bpart, s),
+                       "backward wgrad");
+            }
+            {
+                MarfProfScope ps("wgrad_reduce", s);
+                HIPCHK(marf_launch_wgrad_reduce(part, bpart, wp.n_chunks, net->Mp[l], net->Kp[l], net->dims[l + 1],
+                                                net->dims[l], d_dparams + net->w_off[l], d_dparams + net->b_off[l], s),
+                       "backward wgrad reduce");
+            }
+        }
+        const int l = nl - 1;
+        {
+            MarfProfScope ps("wgrad_last", s);
+            HIPCHK(marf_launch_wgrad_last(net->dtype, a.glast, sv + sp.feat[l], a.S, net->Kp[l], net->Kp[l], wp.chunk,
+                                          wp.n_chunks, part, bpart, s),
+                   "backward wgrad last");
+        }
+        HIPCHK(marf_launch_wgrad_reduce(part, bpart, wp.n_chunks, 3, net->Kp[l], 3, net->dims[l],
+                                        d_dparams + net->w_off[l], d_dparams + net->b_off[l], s),
+               "backward wgrad last reduce");
+    }
+    if (a.geo.mode == MARF_GEO_GRID && d_dh) {
+        MarfProfScope ps("warp_bwd", s);
+        HIPCHK(marf_launch_reduce_dH(a.dH_partial, a.geo.Np_pad / net->TP, a.geo.B, d_h_params, nullptr, d_dh,
+                                     lie_batch > 0 ? lie_batch : a.geo.B, s),
+               "backward warp");
+    }
+    return MARF_OK;
+}
+
+// ------------------------------------------------------------------ loss / optimizer
+
+size_t marf_mse_workspace_bytes(void) { return 1024 * 2 * sizeof(double); }
+
+int marf_masked_mse(const float* d_pred, const float* d_gt, const float* d_mask, int B, int Np,
+                    const float* d_denom_override, float* d_out, void* d_ws, void* stream) {
+    if (B <= 0 || Np <= 0 || !d_pred || !d_gt || !d_out || !d_ws) return fail(MARF_ERR_INVALID, "masked_mse: bad args");
+    MarfProfScope ps("loss_fwd", (hipStream_t)stream);
+    HIPCHK(marf_launch_mse(d_pred, d_gt, d_mask, B, Np, (double*)d_ws, d_out, d_denom_override, (hipStream_t)stream),
+           "masked_mse");
+    return MARF_OK;
+}
+
+int marf_masked_mse_backward(const float* d_pred, const float* d_gt, const float* d_mask, int B, int Np,
+                             const float* d_denom, const float* d_gout, float* d_dpred, void* stream) {
+    if (B <= 0 || Np <= 0 || !d_pred || !d_gt || !d_denom || !d_gout || !d_dpred)
+        return fail(MARF_ERR_INVALID, "masked_mse_backward: bad args");
+    MarfProfScope ps("loss_bwd", (hipStream_t)stream);
+    HIPCHK(marf_launch_mse_bwd(d_pred, d_gt, d_mask, B, Np, d_denom, d_gout, d_dpred, (hipStream_t)stream),
+           "masked_mse_backward");
+    return MARF_OK;
+}
+
+int marf_adam_step(float* d_p, const float* d_g, float* d_m, float* d_v, long long n, double lr, double beta1,
+                   double beta2, double eps, long long step, const float* d_grad_scale, void* stream) {
+    if (n < 0 || step < 1 || (n > 0 && (!d_p || !d_g || !d_m || !d_v))) return fail(MARF_ERR_INVALID, "adam: bad args");
+    // torch.optim.Adam: bias corrections in python float64, step_size = lr / bc1, bc2 ** 0.5
+    double bc1 = 1.0 - std::pow(beta1, (double)step);
+    double bc2 = 1.0 - std::pow(beta2, (double)step);
+    double step_size = lr / bc1;
+    double bc2_sqrt = std::sqrt(bc2);
+    MarfProfScope ps("adam", (hipStream_t)stream);
+    HIPCHK(marf_launch_adam(d_p, d_g, d_m, d_v, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
+                            (float)step_size, (float)bc2_sqrt, (float)eps, d_grad_scale, (hipStream_t)stream),
+           "adam");
+    return MARF_OK;
+}
+
+}  // extern "C"

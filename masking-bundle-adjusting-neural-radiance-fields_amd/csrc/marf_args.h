@@ -1,0 +1,78 @@
+// marf_args.h -- kernel argument blocks and host launcher prototypes shared by the .hip units.
+#pragma once
+#include "marf_common.h"
+
+namespace marf {
+
+struct C2fDev {
+    const float* progress;  // device scalar (NeuralImageFunction.progress)
+    float start, span;      // barf_c2f start, end - start
+    int on;
+};
+
+struct FwdArgs {
+    NetDev net;
+    GeoDev geo;
+    C2fDev c2f;
+    float* rgb;                       // [B][Np][3]
+    void* feat[MARF_MAX_LAYERS];      // saved layer inputs [S][Kp_l] (nullptr: do not save)
+    uint32_t* mask[MARF_MAX_LAYERS];  // relu masks of feat_l (l >= 1) [Kp_l/32][S]
+    long long S;
+    int lda;                          // LDS row stride (elements)
+};
+
+struct BwdArgs {
+    NetDev net;
+    GeoDev geo;
+    C2fDev c2f;
+    const float* rgb;                       // [B][Np][3] forward output
+    const float* d_rgb;                     // [B][Np][3]
+    const uint32_t* mask[MARF_MAX_LAYERS];  // from forward
+    void* dz[MARF_MAX_LAYERS];              // out: dz_l (l >= 1) [S][Kp_l] (grad of layer l-1 pre-act)
+    float* glast;                           // out: [S][4] grad of the last layer pre-activation
+    float* dH_partial;                      // out (geo mode 0): [n_tiles][9]
+    float* d_coords;                        // out (geo mode 1): [Np][2] (may be null)
+    long long S;
+    int lda;
+};
+
+struct PackLayer {
+    int M, K;                            // true dims (nn.Linear weight [M][K])
+    int Mp, Kp, Mt;                      // padded: Wf [Mp][Kp], Wt [Kp][Mt], bias [Mp]
+    long long w_off, b_off;              // offsets in the flat fp32 parameter vector
+    long long wf_off, wt_off, bias_off;  // byte offsets in the packed buffer
+};
+
+struct PackArgs {
+    int n_layers;
+    PackLayer ly[MARF_MAX_LAYERS];
+};
+
+}  // namespace marf
+
+hipError_t marf_launch_sl3(const float* h, float* H, int B, int batch_hint, hipStream_t s);
+hipError_t marf_launch_sl3_bwd(const float* h, const float* dH, float* dh, int B, int batch_hint, hipStream_t s);
+hipError_t marf_launch_reduce_dH(const float* partial, int tiles_per_patch, int B, const float* h, float* dH_out,
+                                 float* dh, int batch_hint, hipStream_t s);
+hipError_t marf_launch_mlp_fwd(const marf::FwdArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
+hipError_t marf_launch_mlp_bwd(const marf::BwdArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
+hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
+                             int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s);
+hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* feat, long long S, int ldf, int K,
+                                  int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s);
+hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
+                                    int Ko, float* dW, float* db, hipStream_t s);
+hipError_t marf_launch_mse(const float* pred, const float* gt, const float* mask, int B, int Np, double* part,
+                           float* out, const float* denom_override, hipStream_t s);
+hipError_t marf_launch_mse_bwd(const float* pred, const float* gt, const float* mask, int B, int Np,
+                               const float* denom, const float* gout, float* d_pred, hipStream_t s);
+hipError_t marf_launch_adam(float* p, const float* g, float* m, float* v, long long n, float w1, float b2,
+                            float one_minus_b2, float step_size, float bc2_sqrt, float eps, const float* grad_scale,
+                            hipStream_t s);
+hipError_t marf_launch_pack(int dtype, const float* params, char* packed, const marf::PackArgs& a,
+                            long long max_elems, hipStream_t s);
+hipError_t marf_launch_pixel_grid(const GeoDev& g, float* xy, int n, hipStream_t s);
+hipError_t marf_launch_warp_points(const float* xy, const float* Hm, float* uv, int B, int n, int xy_shared,
+                                   hipStream_t s);
+hipError_t marf_launch_posenc(const float* coord, long long n, int L, const float* progress, float start, float span,
+                              int c2f_on, float* enc, hipStream_t s);

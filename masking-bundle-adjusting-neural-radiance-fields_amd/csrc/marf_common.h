@@ -1,0 +1,187 @@
+// marf_common.h -- shared device-side definitions for the MI355X (gfx950) planar BA kernels.
+//
+// Layout conventions (see DESIGN.md "Data layout in HBM"):
+//   * pixel slots s = b * Np_pad + p  (patch b, pixel p row-major in the crop, Np_pad = Np rounded
+//     up to MARF_TILE_PAD); slots with p >= Np are padding (never written to user outputs, zero
+//     gradient).
+//   * saved activations  feat_l : [S][Kp_l]  (storage type T, pixel-major rows)
+//   * relu masks         mask_l : [Kp_l/32][S] uint32, bit j of word t <-> feature 32t+j > 0
+//   * packed weights     Wf_l   : [Mp_l][Kp_l] T (forward A operand, nn.Linear row layout, zero pad)
+//                        Wt_l   : [Kp_l][Mt_l] T (transposed, backward A operand)
+//   * MFMA 32x32 accumulator map (both dtypes): lane l, reg r -> col = l&31,
+//     row = (r&3) + 8*(r>>2) + 4*(l>>5).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MARF_TILE_PAD 128  // pixel-count granularity of every per-patch slot range
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+#define MARF_DEV __device__ __forceinline__
+
+// ------------------------------------------------------------------ bf16 helpers
+
+MARF_DEV u16 f2bf(float x) {
+    // round-to-nearest-even, NaN kept NaN (matches torch's float->bfloat16 conversion)
+    uint32_t u = __float_as_uint(x);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (u16)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (u16)(u >> 16);
+}
+MARF_DEV float bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// ------------------------------------------------------------------ precision traits
+
+// bf16: v_mfma_f32_32x32x16_bf16. A/B fragment of a 16-deep k-step: lane l holds
+// A[row l&31][k0 + 8*(l>>5) + j], B[k0 + 8*(l>>5) + j][col l&31], j = 0..7 (16 bytes).
+struct PrecBF16 {
+    typedef u16 T;
+    static constexpr int KS = 16;       // k per MFMA (32x32 shape)
+    static constexpr int KS16 = 32;     // k per MFMA (16x16 shape)
+    typedef bf16x8 frag;
+    static constexpr int kDtype = 1;
+
+    MARF_DEV static frag load_frag(const T* p) {  // 8 contiguous bf16 (16-B aligned)
+        return *reinterpret_cast<const frag*>(p);
+    }
+    MARF_DEV static int kofs(int lane) { return 8 * (lane >> 5); }    // 32x32 k offset
+    MARF_DEV static int kofs16(int lane) { return 8 * (lane >> 4); }  // 16x16 k offset
+    MARF_DEV static f32x16 mma32(frag a, frag b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+    MARF_DEV static f32x4 mma16(frag a, frag b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+    MARF_DEV static T cvt(float x) { return f2bf(x); }
+    MARF_DEV static float tof(T x) { return bf2f(x); }
+};
+
+// fp32: v_mfma_f32_32x32x2_f32 (exact fp32 fma chain). Lane l holds A[row l&31][k0 + (l>>5)],
+// B[k0 + (l>>5)][col l&31].  16x16 form: v_mfma_f32_16x16x4_f32, k0 + (l>>4).
+struct PrecF32 {
+    typedef float T;
+    static constexpr int KS = 2;
+    static constexpr int KS16 = 4;
+    typedef float frag;
+    static constexpr int kDtype = 0;
+
+    MARF_DEV static frag load_frag(const T* p) { return *p; }
+    MARF_DEV static int kofs(int lane) { return lane >> 5; }
+    MARF_DEV static int kofs16(int lane) { return lane >> 4; }
+    MARF_DEV static f32x16 mma32(frag a, frag b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+    }
+    MARF_DEV static f32x4 mma16(frag a, frag b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    MARF_DEV static T cvt(float x) { return x; }
+    MARF_DEV static float tof(T x) { return x; }
+};
+
+// Row of the 32x32 accumulator element (lane, reg).
+MARF_DEV int acc_row(int lane, int r) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// ------------------------------------------------------------------ network descriptor
+
+#define MARF_MAX_LAYERS 10
+
+struct NetDev {
+    int n_layers;                  // Linear layers
+    int L;                         // posenc bands (0 = posenc off)
+    int D;                         // input features 2 + 4L (or 2)
+    int Kp[MARF_MAX_LAYERS];       // padded input width of layer l (Kp[0] = padded D)
+    int Mp[MARF_MAX_LAYERS];       // padded output width of layer l (hidden: mult of 32; last: 16)
+    int Mt[MARF_MAX_LAYERS];       // padded k-width of Wt_l (= Mp for hidden, 16 for last)
+    const void* Wf[MARF_MAX_LAYERS];  // packed forward weights (T)
+    const void* Wt[MARF_MAX_LAYERS];  // packed transposed weights (T)
+    const float* bias[MARF_MAX_LAYERS];  // padded fp32 bias [Mp]
+};
+
+// Geometry of the pixel source.
+struct GeoDev {
+    int mode;       // 0 = crop grid warped by per-patch H; 1 = explicit coordinates
+    int B;          // patches (mode 1: 1)
+    int Np;         // valid pixels per patch
+    int Np_pad;     // slot stride per patch (multiple of MARF_TILE_PAD)
+    int H, W;       // canvas
+    int x0, y0, w;  // crop origin and crop width (row-major p = r*w + c)
+    float norm_h, norm_w;
+    const float* Hm;      // [B][9] (mode 0)
+    const float* coords;  // [Np][2] (mode 1)
+    int bmm_small;        // torch's small-bmm rounding (3 * Np * 3 < 400)
+};
+
+// warp.py:38-43: ((i + 0.5) / max * 2 - 1) * norm in fp32 with IEEE division (the library is
+// compiled with -ffp-contract=off so no step is fused).
+MARF_DEV float grid_coord(int i, int maxdim, float norm) {
+    float t = (float)i + 0.5f;
+    t = t / (float)maxdim;
+    t = t * 2.0f;
+    t = t - 1.0f;
+    return t * norm;
+}
+
+// warp.py:74-78 as torch-CPU's bmm evaluates it.  For a point set with 3*n*3 >= 400 torch runs the
+// BLAS path: acc = x*H0; acc = fma(y, H1, acc); acc += H2.  Below that size torch's small-matrix
+// kernel accumulates with separate multiply and add (bmm_small = 1).
+MARF_DEV void warp_point(const float* Hm, float x, float y, float& u, float& v, float* X, int bmm_small = 0) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        float acc = x * Hm[3 * r + 0];
+        if (bmm_small) acc = acc + y * Hm[3 * r + 1];
+        else acc = __fmaf_rn(y, Hm[3 * r + 1], acc);
+        acc = acc + Hm[3 * r + 2];
+        X[r] = acc;
+    }
+    float d = X[2] + 1e-8f;
+    u = X[0] / d;
+    v = X[1] / d;
+}
+
+// Pixel slot -> (x, y) grid point and warped (u, v).  Returns false for padding slots.
+MARF_DEV bool slot_point(const GeoDev& g, int b, int p, float& x, float& y, float& u, float& v, float* X) {
+    if (p >= g.Np) return false;
+    if (g.mode == 1) {
+        u = g.coords[2 * (size_t)p];
+        v = g.coords[2 * (size_t)p + 1];
+        x = u;
+        y = v;
+        X[0] = u; X[1] = v; X[2] = 1.0f;
+        return true;
+    }
+    int r = p / g.w, c = p - r * g.w;
+    x = grid_coord(g.x0 + c, g.W, g.norm_w);
+    y = grid_coord(g.y0 + r, g.H, g.norm_h);
+    warp_point(g.Hm + 9 * b, x, y, u, v, X, g.bmm_small);
+    return true;
+}
+
+// BARF coarse-to-fine weight of band k (model/planar.py:462-467).
+MARF_DEV float c2f_weight(float progress, float start, float end_minus_start, int L, int k) {
+    const float pi_f = 3.14159265358979323846f;
+    float a = progress - start;
+    a = a / end_minus_start;
+    a = a * (float)L;
+    float t = a - (float)k;
+    t = fminf(fmaxf(t, 0.0f), 1.0f);
+    t = t * pi_f;
+    t = cosf(t);
+    return (1.0f - t) / 2.0f;
+}
+
+// Posenc argument 2^k * fl(c * pi_f32), bit-identical to fl(c * fl(2^k * pi_f32)).
+MARF_DEV float posenc_arg(float c, int k) {
+    const float pi_f = 3.14159265358979323846f;
+    return ldexpf(c * pi_f, k);
+}
+
+MARF_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}

@@ -1,0 +1,238 @@
+// marf_misc.hip -- the small kernels around the hot loop:
+//   * masked MSE forward/backward            (Graph.mse_loss, model/planar.py:382-391)
+//   * Adam                                   (torch.optim.Adam as built in Model.setup_optimizer,
+//                                             model/planar.py:86-104)
+//   * weight packing fp32 master -> bf16/fp32 MFMA operand layouts (padded, + transposed copy)
+//   * standalone pixel grid / warp / posenc  (warp.py:33-81, model/planar.py:451-471) for the
+//     module-level API (Warp.get_normalized_pixel_grid, Warp.warp_grid,
+//     NeuralImageFunction.positional_encoding)
+#include "marf_args.h"
+
+namespace marf {
+
+// ------------------------------------------------------------------ masked MSE
+
+// pred [B][Np][3] (pixel-major, as the MLP writes it), gt [B][3][h*w], mask [B][1][h*w] (or null).
+// Per-block partial sums in fp64: num = sum ((pred-gt)*m)^2, msum = sum m.
+__global__ void k_mse_partial(const float* __restrict__ pred, const float* __restrict__ gt,
+                              const float* __restrict__ mask, int B, int Np, double* __restrict__ part) {
+    __shared__ double rn[256], rm[256];
+    double num = 0.0, ms = 0.0;
+    const long long n = (long long)B * Np;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        int b = (int)(e / Np), p = (int)(e % Np);
+        float m = mask ? mask[(size_t)b * Np + p] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float d = (pred[e * 3 + c] - gt[((size_t)b * 3 + c) * Np + p]) * m;
+            float d2 = d * d;
+            num += (double)d2;
+        }
+        ms += (double)m;
+    }
+    rn[threadIdx.x] = num;
+    rm[threadIdx.x] = ms;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            rn[threadIdx.x] += rn[threadIdx.x + o];
+            rm[threadIdx.x] += rm[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = rn[0];
+        part[2 * blockIdx.x + 1] = rm[0];
+    }
+}
+
+// loss = f32(num) / (f32(sum m) * 3)   (model/planar.py:390); out[0] = loss, out[1] = denominator.
+// denom_override (device scalar, optional): the global 3*sum(mask) when the patches are sharded over
+// ranks (each rank then returns its share of the global loss).
+__global__ void k_mse_final(const double* __restrict__ part, int nblk, float* __restrict__ out,
+                            const float* __restrict__ denom_override) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double num = 0.0, ms = 0.0;
+    for (int i = 0; i < nblk; ++i) {
+        num += part[2 * i];
+        ms += part[2 * i + 1];
+    }
+    float denom = denom_override ? denom_override[0] : (float)ms * 3.0f;
+    out[0] = (float)num / denom;
+    out[1] = denom;
+    out[2] = (float)ms * 3.0f;
+}
+
+// d pred = ((gout / denom) * (2 * (pred - gt) * m)) * m   (autograd of model/planar.py:388-390)
+__global__ void k_mse_backward(const float* __restrict__ pred, const float* __restrict__ gt,
+                               const float* __restrict__ mask, int B, int Np, const float* __restrict__ denom,
+                               const float* __restrict__ gout, float* __restrict__ d_pred) {
+    const long long n = (long long)B * Np;
+    const float gs = gout[0] / denom[0];
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        int b = (int)(e / Np), p = (int)(e % Np);
+        float m = mask ? mask[(size_t)b * Np + p] : 1.0f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float md = (pred[e * 3 + c] - gt[((size_t)b * 3 + c) * Np + p]) * m;
+            d_pred[e * 3 + c] = (gs * (2.0f * md)) * m;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ Adam
+
+// torch.optim.Adam (foreach form): m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g g;
+// p -= step_size * m / (sqrt(v) / sqrt(bc2) + eps).  grad_scale multiplies g first (1 = none).
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, long long n, float w1, float b2, float one_minus_b2,
+                       float step_size, float bc2_sqrt, float eps, const float* __restrict__ grad_scale) {
+    const float gsc = grad_scale ? grad_scale[0] : 1.0f;
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        float gi = g[i] * gsc;
+        float mi = m[i];
+        mi = mi + w1 * (gi - mi);
+        float vi = v[i] * b2;
+        vi = vi + one_minus_b2 * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        float denom = sqrtf(vi) / bc2_sqrt + eps;
+        p[i] = p[i] - step_size * (mi / denom);
+    }
+}
+
+// ------------------------------------------------------------------ packing
+
+template <class P>
+__global__ void k_pack(const float* __restrict__ params, char* __restrict__ packed, PackArgs a) {
+    typedef typename P::T T;
+    const int l = blockIdx.y;
+    const PackLayer& L = a.ly[l];
+    T* wf = reinterpret_cast<T*>(packed + L.wf_off);
+    T* wt = reinterpret_cast<T*>(packed + L.wt_off);
+    float* bias = reinterpret_cast<float*>(packed + L.bias_off);
+    const float* W = params + L.w_off;
+    const float* bsrc = params + L.b_off;
+    const long long nf = (long long)L.Mp * L.Kp;
+    const long long nt = (long long)L.Kp * L.Mt;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < nf + nt + L.Mp; e += (long long)gridDim.x * 256) {
+        if (e < nf) {
+            int m = (int)(e / L.Kp), k = (int)(e % L.Kp);
+            wf[e] = P::cvt(m < L.M && k < L.K ? W[(size_t)m * L.K + k] : 0.f);
+        } else if (e < nf + nt) {
+            long long f = e - nf;
+            int k = (int)(f / L.Mt), m = (int)(f % L.Mt);
+            wt[f] = P::cvt(m < L.M && k < L.K ? W[(size_t)m * L.K + k] : 0.f);
+        } else {
+            int m = (int)(e - nf - nt);
+            bias[m] = m < L.M ? bsrc[m] : 0.f;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ standalone prologue ops
+
+__global__ void k_pixel_grid(GeoDev g, float* __restrict__ xy, int n) {
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
+        int r = p / g.w, c = p - r * g.w;
+        xy[2 * (size_t)p] = grid_coord(g.x0 + c, g.W, g.norm_w);
+        xy[2 * (size_t)p + 1] = grid_coord(g.y0 + r, g.H, g.norm_h);
+    }
+}
+
+// xy [B or 1][n][2] -> uv [B][n][2] under Hm [B][9]
+__global__ void k_warp_points(const float* __restrict__ xy, const float* __restrict__ Hm, float* __restrict__ uv,
+                              int B, int n, int xy_shared) {
+    const long long tot = (long long)B * n;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < tot; e += (long long)gridDim.x * 256) {
+        int b = (int)(e / n);
+        long long src = xy_shared ? (e % n) : e;
+        float X[3], u, v;
+        warp_point(Hm + 9 * b, xy[2 * src], xy[2 * src + 1], u, v, X, 9 * n < 400);
+        uv[2 * e] = u;
+        uv[2 * e + 1] = v;
+    }
+}
+
+// coord [n][2] -> enc [n][4L] (model/planar.py:451-471 layout: x: sin_k, cos_k; y: sin_k, cos_k)
+__global__ void k_posenc(const float* __restrict__ coord, long long n, int L, const float* progress, float start,
+                         float span, int c2f_on, float* __restrict__ enc) {
+    const long long tot = n * 2 * L;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < tot; e += (long long)gridDim.x * 256) {
+        long long i = e / (2 * L);
+        int ck = (int)(e % (2 * L)), c = ck / L, k = ck % L;
+        float s, co;
+        sincosf(posenc_arg(coord[2 * i + c], k), &s, &co);
+        if (c2f_on) {
+            float w = c2f_weight(*progress, start, span, L, k);
+            s = s * w;
+            co = co * w;
+        }
+        enc[i * 4 * L + c * 2 * L + k] = s;
+        enc[i * 4 * L + c * 2 * L + L + k] = co;
+    }
+}
+
+}  // namespace marf
+
+using namespace marf;
+
+static int grid_for(long long n) {
+    long long b = (n + 255) / 256;
+    if (b > 8192) b = 8192;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
+hipError_t marf_launch_mse(const float* pred, const float* gt, const float* mask, int B, int Np, double* part,
+                           float* out, const float* denom_override, hipStream_t s) {
+    int nb = grid_for((long long)B * Np);
+    if (nb > 1024) nb = 1024;
+    hipLaunchKernelGGL(k_mse_partial, dim3(nb), dim3(256), 0, s, pred, gt, mask, B, Np, part);
+    hipLaunchKernelGGL(k_mse_final, dim3(1), dim3(64), 0, s, part, nb, out, denom_override);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_mse_bwd(const float* pred, const float* gt, const float* mask, int B, int Np,
+                               const float* denom, const float* gout, float* d_pred, hipStream_t s) {
+    hipLaunchKernelGGL(k_mse_backward, dim3(grid_for((long long)B * Np)), dim3(256), 0, s, pred, gt, mask, B, Np,
+                       denom, gout, d_pred);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_adam(float* p, const float* g, float* m, float* v, long long n, float w1, float b2,
+                            float one_minus_b2, float step_size, float bc2_sqrt, float eps, const float* grad_scale,
+                            hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_adam, dim3(grid_for(n)), dim3(256), 0, s, p, g, m, v, n, w1, b2, one_minus_b2, step_size,
+                       bc2_sqrt, eps, grad_scale);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_pack(int dtype, const float* params, char* packed, const PackArgs& a, long long max_elems,
+                            hipStream_t s) {
+    dim3 grid(grid_for(max_elems), a.n_layers);
+    if (dtype == 1)
+        hipLaunchKernelGGL(k_pack<PrecBF16>, grid, dim3(256), 0, s, params, packed, a);
+    else
+        hipLaunchKernelGGL(k_pack<PrecF32>, grid, dim3(256), 0, s, params, packed, a);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_pixel_grid(const GeoDev& g, float* xy, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_pixel_grid, dim3(grid_for(n)), dim3(256), 0, s, g, xy, n);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_warp_points(const float* xy, const float* Hm, float* uv, int B, int n, int xy_shared,
+                                   hipStream_t s) {
+    hipLaunchKernelGGL(k_warp_points, dim3(grid_for((long long)B * n)), dim3(256), 0, s, xy, Hm, uv, B, n, xy_shared);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_posenc(const float* coord, long long n, int L, const float* progress, float start, float span,
+                              int c2f_on, float* enc, hipStream_t s) {
+    hipLaunchKernelGGL(k_posenc, dim3(grid_for(n * 2 * L)), dim3(256), 0, s, coord, n, L, progress, start, span,
+                       c2f_on, enc);
+    return hipGetLastError();
+}

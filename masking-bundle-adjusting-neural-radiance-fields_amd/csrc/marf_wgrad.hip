@@ -1,0 +1,311 @@
+// marf_wgrad.hip -- weight gradients of the neural-image MLP, dW_l = sum_px dz_{l+1} (x) feat_l,
+// db_l = sum_px dz_{l+1}  (autograd of nn.Linear, model/planar.py:443).
+//
+// A GEMM whose reduction axis is the pixel axis (K = B*h*w, millions).  Split-K: block (c, o)
+// reduces pixel chunk c into a private fp32 partial of output block o; a second kernel sums the
+// partials in a fixed order (deterministic, no float atomics).
+//
+// bf16: v_mfma_f32_32x32x16_bf16 with both operands pixel-minor.  dz and feat arrive pixel-major
+// ([S][M], [S][K]), are staged 64 pixels at a time into LDS row-major, and read back with
+// ds_read_b64_tr_b16 (gfx950 hardware transpose: per 16-lane group, 4 rows x 16 columns, delivered
+// column-major), so a lane receives 8 consecutive pixels of one feature.  LDS rows are padded by
+// 64 B so the 4 rows of a transposed read fall in distinct 64-B bank groups.
+// fp32: v_mfma_f32_32x32x2_f32, one element per lane, read straight from the row-major tile.
+//
+// 512 threads = 8 waves as 4 (rows) x 2 (cols); each wave owns RT x CT accumulator tiles.
+#include "marf_args.h"
+
+namespace marf {
+
+struct WgArgs {
+    const void* dz;    // [S][ldz] T
+    const void* feat;  // [S][ldf] T
+    long long S;
+    int ldz, ldf;      // row strides
+    int M, K;          // output rows (<= ldz) and cols (<= ldf)
+    int chunk;         // pixels per chunk (multiple of 64)
+    int n_oblk_c;      // output blocks along K
+    float* partial;    // [n_chunks][M][K]
+    float* bpartial;   // [n_chunks][M] (bias), may be null
+};
+
+template <int RT, int CT>
+struct WgGeo {
+    static constexpr int BM = 4 * RT * 32;
+    static constexpr int BN = 2 * CT * 32;
+};
+
+MARF_DEV i16x4 tr_read(const u16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
+}
+
+template <class P, int RT, int CT>
+__global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
+    typedef typename P::T T;
+    constexpr int BM = WgGeo<RT, CT>::BM, BN = WgGeo<RT, CT>::BN;
+    constexpr int PADE = sizeof(T) == 2 ? 32 : 1;  // row padding (elements)
+    constexpr int LDZ = BM + PADE, LDF = BN + PADE;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* tz = reinterpret_cast<T*>(smem);          // [64][LDZ]
+    T* tf = tz + 64 * LDZ;                        // [64][LDF]
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave >> 1, wc = wave & 1;
+    const int chunk_id = blockIdx.x;
+    const int ob = blockIdx.y;
+    const int m0 = (ob / a.n_oblk_c) * BM, k0 = (ob % a.n_oblk_c) * BN;
+    const long long s_begin = (long long)chunk_id * a.chunk;
+    const long long s_end = min(s_begin + a.chunk, a.S);
+    const bool do_bias = a.bpartial && (ob % a.n_oblk_c) == 0;
+    const T* dz = reinterpret_cast<const T*>(a.dz);
+    const T* ft = reinterpret_cast<const T*>(a.feat);
+
+    f32x16 acc[RT][CT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) acc[i][j] = (f32x16){};
+    float bsum = 0.f;
+
+    for (long long s0 = s_begin; s0 < s_end; s0 += 64) {
+        // ---- stage 64 pixel rows of dz (cols m0..m0+BM) and feat (cols k0..k0+BN)
+        __syncthreads();
+        if (sizeof(T) == 2) {
+            for (int e = threadIdx.x; e < 64 * (BM / 8); e += 512) {
+                int r = e / (BM / 8), c = (e % (BM / 8)) * 8;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (s0 + r < s_end && m0 + c < a.M)
+                    v = *reinterpret_cast<const uint4*>(dz + (s0 + r) * a.ldz + m0 + c);
+                *reinterpret_cast<uint4*>(tz + r * LDZ + c) = v;
+            }
+            for (int e = threadIdx.x; e < 64 * (BN / 8); e += 512) {
+                int r = e / (BN / 8), c = (e % (BN / 8)) * 8;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (s0 + r < s_end && k0 + c < a.K)
+                    v = *reinterpret_cast<const uint4*>(ft + (s0 + r) * a.ldf + k0 + c);
+                *reinterpret_cast<uint4*>(tf + r * LDF + c) = v;
+            }
+        } else {
+            for (int e = threadIdx.x; e < 64 * BM; e += 512) {
+                int r = e / BM, c = e % BM;
+                T v = 0;
+                if (s0 + r < s_end && m0 + c < a.M) v = dz[(s0 + r) * a.ldz + m0 + c];
+                tz[r * LDZ + c] = v;
+            }
+            for (int e = threadIdx.x; e < 64 * BN; e += 512) {
+                int r = e / BN, c = e % BN;
+                T v = 0;
+                if (s0 + r < s_end && k0 + c < a.K) v = ft[(s0 + r) * a.ldf + k0 + c];
+                tf[r * LDF + c] = v;
+            }
+        }
+        __syncthreads();
+
+        if (do_bias) {
+            // db partial: thread t sums column t%BM over rows t/BM, t/BM + 512/BM, ...
+            constexpr int RSTEP = 512 / BM > 0 ? 512 / BM : 1;
+            const int c = threadIdx.x % BM, r0 = threadIdx.x / BM;
+            if (r0 < RSTEP)
+                for (int r = r0; r < 64; r += RSTEP) bsum += P::tof(tz[r * LDZ + c]);
+        }
+
+        if constexpr (sizeof(T) == 2) {
+            const int g = lane >> 4, gi = lane & 15, q = gi >> 2, p4 = gi & 3;
+#pragma unroll
+            for (int ks = 0; ks < 64; ks += 16) {
+                const int r0 = ks + 8 * (g >> 1) + q;  // this lane supplies row r0 (and r0 + 4)
+                typename P::frag af[RT], bf[CT];
+#pragma unroll
+                for (int i = 0; i < RT; ++i) {
+                    const int c0 = (wr * RT + i) * 32 + 16 * (g & 1) + 4 * p4;
+                    const u16* base = reinterpret_cast<const u16*>(tz) + r0 * LDZ + c0;
+                    i16x4 lo = tr_read(base), hi = tr_read(base + 4 * LDZ);
+                    i16x4 v[2] = {lo, hi};
+                    af[i] = *reinterpret_cast<bf16x8*>(v);
+                }
+#pragma unroll
+                for (int j = 0; j < CT; ++j) {
+                    const int c0 = (wc * CT + j) * 32 + 16 * (g & 1) + 4 * p4;
+                    const u16* base = reinterpret_cast<const u16*>(tf) + r0 * LDF + c0;
+                    i16x4 lo = tr_read(base), hi = tr_read(base + 4 * LDF);
+                    i16x4 v[2] = {lo, hi};
+                    bf[j] = *reinterpret_cast<bf16x8*>(v);
+                }
+#pragma unroll
+                for (int i = 0; i < RT; ++i)
+#pragma unroll
+                    for (int j = 0; j < CT; ++j) acc[i][j] = P::mma32(af[i], bf[j], acc[i][j]);
+            }
+        } else {
+            const int h = lane >> 5, rl = lane & 31;
+            for (int ks = 0; ks < 64; ks += 2) {
+                typename P::frag af[RT], bf[CT];
+#pragma unroll
+                for (int i = 0; i < RT; ++i) af[i] = tz[(ks + h) * LDZ + (wr * RT + i) * 32 + rl];
+#pragma unroll
+                for (int j = 0; j < CT; ++j) bf[j] = tf[(ks + h) * LDF + (wc * CT + j) * 32 + rl];
+#pragma unroll
+                for (int i = 0; i < RT; ++i)
+#pragma unroll
+                    for (int j = 0; j < CT; ++j) acc[i][j] = P::mma32(af[i], bf[j], acc[i][j]);
+            }
+        }
+    }
+
+    // ---- epilogue: partial[chunk][m][k]
+    float* out = a.partial + (size_t)chunk_id * a.M * a.K;
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) {
+            const int k = k0 + (wc * CT + j) * 32 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + (wr * RT + i) * 32 + acc_row(lane, r);
+                if (m < a.M && k < a.K) out[(size_t)m * a.K + k] = acc[i][j][r];
+            }
+        }
+    if (do_bias) {
+        __syncthreads();
+        float* bs = reinterpret_cast<float*>(smem);
+        bs[threadIdx.x] = bsum;
+        __syncthreads();
+        constexpr int RSTEP = 512 / BM > 0 ? 512 / BM : 1;
+        if ((int)threadIdx.x < BM && m0 + (int)threadIdx.x < a.M) {
+            float s = 0.f;
+            for (int r = 0; r < RSTEP; ++r) s += bs[threadIdx.x + r * BM];
+            a.bpartial[(size_t)chunk_id * a.M + m0 + threadIdx.x] = s;
+        }
+    }
+}
+
+// Last layer (3 outputs): dW[c][k] = sum_px g[px][c] feat[px][k] on the VALU (K <= 1024).
+template <class P>
+__global__ __launch_bounds__(256) void k_wgrad_last(const float* __restrict__ glast, const void* feat_v, long long S,
+                                                    int ldf, int K, int chunk, float* partial, float* bpartial) {
+    typedef typename P::T T;
+    const T* feat = reinterpret_cast<const T*>(feat_v);
+    const long long s_begin = (long long)blockIdx.x * chunk;
+    const long long s_end = min(s_begin + chunk, S);
+    float acc[4][3];
+    for (int j = 0; j < 4; ++j)
+        for (int c = 0; c < 3; ++c) acc[j][c] = 0.f;
+    float bs[3] = {0.f, 0.f, 0.f};
+    for (long long s = s_begin; s < s_end; ++s) {
+        float4 g = *reinterpret_cast<const float4*>(glast + s * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int k = threadIdx.x + 256 * j;
+            if (k < K) {
+                float f = P::tof(feat[s * ldf + k]);
+                acc[j][0] += g.x * f;
+                acc[j][1] += g.y * f;
+                acc[j][2] += g.z * f;
+            }
+        }
+        bs[0] += g.x;
+        bs[1] += g.y;
+        bs[2] += g.z;
+    }
+    float* out = partial + (size_t)blockIdx.x * 3 * K;
+    for (int j = 0; j < 4; ++j) {
+        int k = threadIdx.x + 256 * j;
+        if (k < K)
+            for (int c = 0; c < 3; ++c) out[c * K + k] = acc[j][c];
+    }
+    if (threadIdx.x == 0)
+        for (int c = 0; c < 3; ++c) bpartial[(size_t)blockIdx.x * 3 + c] = bs[c];
+}
+
+// Fixed-order sum of the chunk partials into the flat fp32 gradient (nn.Linear layout [M][K],
+// unpadded [Mo][Ko]), then the bias.
+__global__ void k_wgrad_reduce(const float* __restrict__ partial, const float* __restrict__ bpartial, int n_chunks,
+                               int M, int K, int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db) {
+    const long long n = (long long)Mo * Ko;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n + Mo;
+         e += (long long)gridDim.x * blockDim.x) {
+        if (e < n) {
+            int m = (int)(e / Ko), k = (int)(e % Ko);
+            float s = 0.f;
+            for (int c = 0; c < n_chunks; ++c) s += partial[((size_t)c * M + m) * K + k];
+            dW[e] = s;
+        } else {
+            int m = (int)(e - n);
+            float s = 0.f;
+            for (int c = 0; c < n_chunks; ++c) s += bpartial[(size_t)c * M + m];
+            db[m] = s;
+        }
+    }
+}
+
+}  // namespace marf
+
+using namespace marf;
+
+template <class P, int RT, int CT>
+static hipError_t launch_wg(const WgArgs& a, int n_chunks, int n_oblk, hipStream_t s) {
+    typedef typename P::T T;
+    constexpr int BM = WgGeo<RT, CT>::BM, BN = WgGeo<RT, CT>::BN;
+    constexpr int PADE = sizeof(T) == 2 ? 32 : 1;
+    size_t lds = (size_t)64 * (BM + PADE + BN + PADE) * sizeof(T);
+    if (lds < 512 * sizeof(float)) lds = 512 * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_wgrad<P, RT, CT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_wgrad<P, RT, CT>), dim3(n_chunks, n_oblk), dim3(512), lds, s, a);
+    return hipGetLastError();
+}
+
+// Picks the output-block shape for an M x K weight gradient: 256x256 (2x4 tiles per wave),
+// 256x64 (2x1) or 128x64 (1x1).
+hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
+                             int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s) {
+    WgArgs a;
+    a.dz = dz;
+    a.feat = feat;
+    a.S = S;
+    a.ldz = ldz;
+    a.ldf = ldf;
+    a.M = M;
+    a.K = K;
+    a.chunk = chunk;
+    a.partial = partial;
+    a.bpartial = bpartial;
+    int cfg;
+    if (M >= 256 && K >= 192) cfg = 0;
+    else if (M >= 256) cfg = 1;
+    else cfg = 2;
+    int BM = cfg == 2 ? 128 : 256, BN = cfg == 0 ? 256 : 64;
+    int nr = (M + BM - 1) / BM, nc = (K + BN - 1) / BN;
+    a.n_oblk_c = nc;
+    if (dtype == 1) {
+        if (cfg == 0) return launch_wg<PrecBF16, 2, 4>(a, n_chunks, nr * nc, s);
+        if (cfg == 1) return launch_wg<PrecBF16, 2, 1>(a, n_chunks, nr * nc, s);
+        return launch_wg<PrecBF16, 1, 1>(a, n_chunks, nr * nc, s);
+    }
+    if (cfg == 0) return launch_wg<PrecF32, 2, 4>(a, n_chunks, nr * nc, s);
+    if (cfg == 1) return launch_wg<PrecF32, 2, 1>(a, n_chunks, nr * nc, s);
+    return launch_wg<PrecF32, 1, 1>(a, n_chunks, nr * nc, s);
+}
+
+hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* feat, long long S, int ldf, int K, int chunk,
+                                  int n_chunks, float* partial, float* bpartial, hipStream_t s) {
+    if (dtype == 1)
+        hipLaunchKernelGGL(k_wgrad_last<PrecBF16>, dim3(n_chunks), dim3(256), 0, s, glast, feat, S, ldf, K, chunk,
+                           partial, bpartial);
+    else
+        hipLaunchKernelGGL(k_wgrad_last<PrecF32>, dim3(n_chunks), dim3(256), 0, s, glast, feat, S, ldf, K, chunk,
+                           partial, bpartial);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
+                                    int Ko, float* dW, float* db, hipStream_t s) {
+    long long n = (long long)Mo * Ko + Mo;
+    int blocks = (int)((n + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, s, partial, bpartial, n_chunks, M, K, Mo, Ko, dW, db);
+    return hipGetLastError();
+}

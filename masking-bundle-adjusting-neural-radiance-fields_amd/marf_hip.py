@@ -1,0 +1,553 @@
+"""ctypes binding of libmarf.so (include/marf.h) and the autograd functions built on it.
+
+This is the only module that talks to the HIP library.  PyTorch is used for device memory
+(caching allocator), the current HIP stream and autograd bookkeeping; every arithmetic step of
+the planar render loop runs in the library's kernels.  There is no CPU or eager-PyTorch fallback:
+if the library is missing or the tensors are not on a ROCm device the calls raise.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmarf.so")
+
+MARF_FP32, MARF_BF16 = 0, 1
+GEO_GRID, GEO_COORDS = 0, 1
+
+_c_int, _c_ll, _c_dbl, _c_vp, _c_sz = ctypes.c_int, ctypes.c_longlong, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
+
+
+class Geometry(ctypes.Structure):
+    _fields_ = [("mode", _c_int), ("B", _c_int), ("Np", _c_int), ("H", _c_int), ("W", _c_int),
+                ("patch_H", _c_int), ("patch_W", _c_int), ("d_H", _c_vp), ("d_coords", _c_vp)]
+
+
+class C2f(ctypes.Structure):
+    _fields_ = [("d_progress", _c_vp), ("start", _c_dbl), ("end", _c_dbl), ("on", _c_int)]
+
+
+_SIGS = {
+    "marf_last_error": (ctypes.c_char_p, []),
+    "marf_version": (_c_int, []),
+    "marf_sl3_to_SL3": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_vp]),
+    "marf_sl3_to_SL3_backward": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp]),
+    "marf_pixel_grid": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_vp, _c_vp]),
+    "marf_warp_points": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp]),
+    "marf_posenc": (_c_int, [_c_vp, _c_ll, _c_int, ctypes.POINTER(C2f), _c_vp, _c_vp]),
+    "marf_net_create": (_c_int, [_c_int, ctypes.POINTER(_c_int), _c_int, _c_int, ctypes.POINTER(_c_vp)]),
+    "marf_net_destroy": (None, [_c_vp]),
+    "marf_net_param_count": (_c_ll, [_c_vp]),
+    "marf_net_packed_bytes": (_c_sz, [_c_vp]),
+    "marf_net_pack": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp]),
+    "marf_saved_bytes": (_c_sz, [_c_vp, ctypes.POINTER(Geometry)]),
+    "marf_workspace_bytes": (_c_sz, [_c_vp, ctypes.POINTER(Geometry)]),
+    "marf_forward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_vp, _c_vp, _c_vp, _c_vp]),
+    "marf_backward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_vp, _c_vp, _c_int, _c_vp,
+                               _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "marf_mse_workspace_bytes": (_c_sz, []),
+    "marf_masked_mse": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "marf_masked_mse_backward": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "marf_adam_step": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_ll, _c_dbl, _c_dbl, _c_dbl, _c_dbl, _c_ll, _c_vp,
+                                _c_vp]),
+    "marf_profile_enable": (_c_int, [_c_int]),
+    "marf_profile_reset": (_c_int, []),
+    "marf_profile_read": (_c_int, [ctypes.c_char_p, _c_int, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_ll), _c_int]),
+}
+
+_lib = None
+
+# Bumped by every in-library parameter update (marf Adam writes through raw pointers, which torch's
+# version counters do not see); Engine.packed_for re-packs when it changes.
+PARAM_GENERATION = [0]
+
+
+def lib():
+    """Load libmarf.so (building it first if the sources are newer and hipcc is present)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            try:
+                import build_lib
+                build_lib.build(verbose=False)
+            except Exception as e:  # pragma: no cover - message path
+                raise RuntimeError(f"libmarf.so not found at {LIB_PATH} and could not be built: {e}") from e
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError("libmarf: " + lib().marf_last_error().decode())
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _dev(t, name):
+    if not t.is_cuda:
+        raise RuntimeError(f"libmarf: {name} must live on a ROCm GPU (got {t.device}); there is no CPU path")
+    return t
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _f32(t, name):
+    _dev(t, name)
+    if t.dtype != torch.float32:
+        raise TypeError(f"libmarf: {name} must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+def profile_enable(on=True):
+    _check(lib().marf_profile_enable(1 if on else 0))
+
+
+def profile_reset():
+    _check(lib().marf_profile_reset())
+
+
+def profile_read():
+    """{kernel name: (total_ms, launches)} recorded with HIP events since the last reset."""
+    cap, nl = 64, 64
+    names = ctypes.create_string_buffer(cap * nl)
+    tot = (_c_dbl * cap)()
+    cnt = (_c_ll * cap)()
+    n = lib().marf_profile_read(names, nl, tot, cnt, cap)
+    out = {}
+    for i in range(n):
+        nm = names.raw[i * nl:(i + 1) * nl].split(b"\0", 1)[0].decode()
+        out[nm] = (tot[i], cnt[i])
+    return out
+
+
+# ====================================================================== Lie / warp / posenc
+
+class _SL3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, lie_batch):
+        h = _f32(h, "h")
+        B = h.shape[0]
+        H = torch.empty(B, 3, 3, device=h.device, dtype=torch.float32)
+        _check(lib().marf_sl3_to_SL3(_ptr(h), _ptr(H), B, lie_batch, _stream(h)))
+        ctx.save_for_backward(h)
+        ctx.lie_batch = lie_batch
+        return H
+
+    @staticmethod
+    def backward(ctx, dH):
+        (h,) = ctx.saved_tensors
+        dH = _f32(dH, "dH")
+        dh = torch.empty_like(h)
+        _check(lib().marf_sl3_to_SL3_backward(_ptr(h), _ptr(dH), _ptr(dh), h.shape[0], ctx.lie_batch, _stream(h)))
+        return dh, None
+
+
+def sl3_to_SL3(h, lie_batch=0):
+    """h [..., 8] -> H [..., 3, 3]  (warp.py:98-106), differentiable."""
+    shp = h.shape[:-1]
+    hb = h.reshape(-1, 8)
+    lb = lie_batch if lie_batch > 0 else hb.shape[0]
+    return _SL3.apply(hb, lb).reshape(*shp, 3, 3)
+
+
+def pixel_grid(H, W, patch_H, patch_W, crop, device):
+    """One copy of Warp.get_normalized_pixel_grid (warp.py:33-68): [h*w, 2]."""
+    if crop:
+        h = (H // 2 + patch_H // 2) - (H // 2 - patch_H // 2)
+        w = (W // 2 + patch_W // 2) - (W // 2 - patch_W // 2)
+    else:
+        h, w = H, W
+    xy = torch.empty(h * w, 2, device=device, dtype=torch.float32)
+    _check(lib().marf_pixel_grid(H, W, patch_H, patch_W, 1 if crop else 0, _ptr(xy), _stream(xy)))
+    return xy
+
+
+def warp_points(xy, Hm):
+    """xy [B or 1, n, 2] warped by Hm [B, 3, 3] -> [B, n, 2] (warp.py:74-78), forward only."""
+    xy = _f32(xy, "xy")
+    Hm = _f32(Hm, "H")
+    B, n = Hm.shape[0], xy.shape[-2]
+    shared = 1 if xy.dim() == 2 or xy.shape[0] == 1 else 0
+    if not shared and xy.shape[0] != B:
+        raise ValueError("warp_points: batch mismatch")
+    uv = torch.empty(B, n, 2, device=xy.device, dtype=torch.float32)
+    _check(lib().marf_warp_points(_ptr(xy), _ptr(Hm), _ptr(uv), B, n, shared, _stream(xy)))
+    return uv
+
+
+def make_c2f(progress, c2f):
+    c = C2f()
+    if c2f is not None and progress is not None:
+        c.d_progress = progress.data_ptr()
+        c.start, c.end, c.on = float(c2f[0]), float(c2f[1]), 1
+    return c
+
+
+def posenc(coord, L, progress=None, c2f=None):
+    """coord [..., 2] -> [..., 4L] (model/planar.py:451-471 layout), forward only."""
+    coord = _f32(coord, "coord")
+    n = coord.numel() // 2
+    enc = torch.empty(*coord.shape[:-1], 4 * L, device=coord.device, dtype=torch.float32)
+    cf = make_c2f(progress, c2f)
+    _check(lib().marf_posenc(_ptr(coord), n, L, ctypes.byref(cf), _ptr(enc), _stream(coord)))
+    return enc
+
+
+# ====================================================================== MLP engine
+
+class Net:
+    """An MLP shape + padding plan in the library (marf_net)."""
+
+    def __init__(self, dims, L, dtype):
+        self.dims = [int(d) for d in dims]
+        self.L = int(L)
+        self.dtype = dtype
+        arr = (_c_int * len(self.dims))(*self.dims)
+        h = _c_vp()
+        _check(lib().marf_net_create(len(self.dims) - 1, arr, self.L, dtype, ctypes.byref(h)))
+        self._h = h
+        self.param_count = lib().marf_net_param_count(h)
+        self.packed_bytes = lib().marf_net_packed_bytes(h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) and _lib is not None:
+                _lib.marf_net_destroy(self._h)
+        except Exception:
+            pass
+
+    def pack(self, flat_params, packed):
+        _check(lib().marf_net_pack(self._h, _ptr(flat_params), _ptr(packed), _stream(flat_params)))
+
+    def saved_bytes(self, geo):
+        return lib().marf_saved_bytes(self._h, ctypes.byref(geo))
+
+    def workspace_bytes(self, geo):
+        return lib().marf_workspace_bytes(self._h, ctypes.byref(geo))
+
+
+def grid_geometry(B, H, W, patch_H, patch_W, Hm=None):
+    g = Geometry()
+    g.mode, g.B, g.H, g.W, g.patch_H, g.patch_W = GEO_GRID, B, H, W, patch_H, patch_W
+    g.d_H = None if Hm is None else Hm.data_ptr()
+    return g
+
+
+def coords_geometry(coords):
+    g = Geometry()
+    g.mode, g.B, g.Np = GEO_COORDS, 1, coords.shape[0]
+    g.d_coords = coords.data_ptr()
+    return g
+
+
+class _Buffers:
+    """Per-device cache of the byte buffers the library borrows (reused across steps)."""
+
+    def __init__(self):
+        self.bufs = {}
+
+    def get(self, name, nbytes, device):
+        t = self.bufs.get(name)
+        if t is None or t.numel() < nbytes or t.device != device:
+            t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+            self.bufs[name] = t
+        return t
+
+
+_BUFS = _Buffers()
+
+
+def _split_grads(flat, shapes):
+    out, off = [], 0
+    for s in shapes:
+        n = 1
+        for d in s:
+            n *= d
+        out.append(flat[off:off + n].view(*s))
+        off += n
+    return out
+
+
+class _MLPFunction(torch.autograd.Function):
+    """NeuralImageFunction.forward on explicit coordinates (model/planar.py:429-449)."""
+
+    @staticmethod
+    def forward(ctx, coords, progress, engine, *params):
+        coords = _f32(coords, "coord_2d")
+        shp = coords.shape[:-1]
+        c2 = coords.reshape(-1, 2)
+        n = c2.shape[0]
+        geo = coords_geometry(c2)
+        rgb = torch.empty(n, 3, device=coords.device, dtype=torch.float32)
+        packed = engine.packed_for(params)
+        need_grad = any(ctx.needs_input_grad)
+        saved = None
+        if need_grad:
+            saved = torch.empty(max(engine.net.saved_bytes(geo), 1), dtype=torch.uint8, device=coords.device)
+        cf = make_c2f(progress, engine.c2f)
+        _check(lib().marf_forward(engine.net.handle, ctypes.byref(geo), ctypes.byref(cf), _ptr(packed), _ptr(rgb),
+                                  _ptr(saved), _stream(coords)))
+        if need_grad:
+            ctx.save_for_backward(c2, progress, rgb)
+            ctx.coord_shape = coords.shape
+            ctx.saved_buf, ctx.packed, ctx.engine = saved, packed, engine
+            ctx.shapes = [p.shape for p in params]
+        return rgb.view(*shp, 3)
+
+    @staticmethod
+    def backward(ctx, d_rgb):
+        c2, progress, rgb = ctx.saved_tensors
+        engine = ctx.engine
+        geo = coords_geometry(c2)
+        d_rgb = _f32(d_rgb, "d_rgb").reshape(-1, 3)
+        ws = _BUFS.get("mlp_ws", engine.net.workspace_bytes(geo), c2.device)
+        dflat = torch.empty(engine.net.param_count, device=c2.device, dtype=torch.float32)
+        dcoords = torch.empty_like(c2) if ctx.needs_input_grad[0] else None
+        cf = make_c2f(progress, engine.c2f)
+        _check(lib().marf_backward(engine.net.handle, ctypes.byref(geo), ctypes.byref(cf), _ptr(ctx.packed), None, 0,
+                                   _ptr(rgb), _ptr(d_rgb), _ptr(ctx.saved_buf), _ptr(ws), _ptr(dflat), None,
+                                   _ptr(dcoords), _stream(c2)))
+        grads = _split_grads(dflat, ctx.shapes)
+        dc = None if dcoords is None else dcoords.view(ctx.coord_shape)
+        return (dc, None, None, *grads)
+
+
+class _PlanarRenderFunction(torch.autograd.Function):
+    """Graph.forward for the training batch (model/planar.py:329-335): crop grid -> sl(3) warp ->
+    posenc/c2f -> MLP, fused in one kernel; backward = dgrad chain + warp adjoint + weight
+    gradients.  Inputs: warp weight [B_all, 8], progress, engine, shard (b0, b1), *mlp params."""
+
+    @staticmethod
+    def forward(ctx, warp_weight, progress, engine, b0, b1, *params):
+        w = _f32(warp_weight, "warp_param")
+        Bl = b1 - b0
+        h_local = w[b0:b1].contiguous()
+        Hm = torch.empty(Bl, 3, 3, device=w.device, dtype=torch.float32)
+        st = _stream(w)
+        _check(lib().marf_sl3_to_SL3(_ptr(h_local), _ptr(Hm), Bl, engine.lie_batch(w.shape[0]), st))
+        geo = engine.grid_geo(Bl, Hm)
+        Np = geo_np(engine)
+        rgb = torch.empty(Bl, Np, 3, device=w.device, dtype=torch.float32)
+        packed = engine.packed_for(params)
+        saved = _BUFS.get("planar_saved", engine.net.saved_bytes(geo), w.device)
+        cf = make_c2f(progress, engine.c2f)
+        _check(lib().marf_forward(engine.net.handle, ctypes.byref(geo), ctypes.byref(cf), _ptr(packed), _ptr(rgb),
+                                  _ptr(saved), st))
+        ctx.save_for_backward(w, progress, rgb)
+        ctx.Hm, ctx.h_local, ctx.saved_buf, ctx.packed, ctx.engine = Hm, h_local, saved, packed, engine
+        ctx.b0, ctx.b1 = b0, b1
+        ctx.shapes = [p.shape for p in params]
+        return rgb
+
+    @staticmethod
+    def backward(ctx, d_rgb):
+        w, progress, rgb = ctx.saved_tensors
+        engine = ctx.engine
+        Bl = ctx.b1 - ctx.b0
+        geo = engine.grid_geo(Bl, ctx.Hm)
+        d_rgb = _f32(d_rgb, "d_rgb")
+        ws = _BUFS.get("planar_ws", engine.net.workspace_bytes(geo), w.device)
+        dflat = torch.empty(engine.net.param_count, device=w.device, dtype=torch.float32)
+        engine.last_flat_grad = dflat
+        dh_local = torch.empty(Bl, 8, device=w.device, dtype=torch.float32)
+        cf = make_c2f(progress, engine.c2f)
+        _check(lib().marf_backward(engine.net.handle, ctypes.byref(geo), ctypes.byref(cf), _ptr(ctx.packed),
+                                   _ptr(ctx.h_local), engine.lie_batch(w.shape[0]), _ptr(rgb), _ptr(d_rgb),
+                                   _ptr(ctx.saved_buf), _ptr(ws), _ptr(dflat), _ptr(dh_local), None, _stream(w)))
+        if Bl == w.shape[0]:
+            dw = dh_local
+        else:
+            dw = torch.zeros_like(w)
+            dw[ctx.b0:ctx.b1] = dh_local
+        grads = _split_grads(dflat, ctx.shapes)
+        return (dw, None, None, None, None, *grads)
+
+
+def geo_np(engine):
+    h = (engine.H // 2 + engine.patch_H // 2) - (engine.H // 2 - engine.patch_H // 2)
+    w = (engine.W // 2 + engine.patch_W // 2) - (engine.W // 2 - engine.patch_W // 2)
+    return h * w
+
+
+class Engine:
+    """Library-side state of one NeuralImageFunction: net plan, packed weights, c2f, geometry."""
+
+    def __init__(self, dims, L, dtype, c2f, H, W, patch_H, patch_W, lie_batch=0):
+        self.net = Net(dims, L, dtype)
+        self.c2f = c2f
+        self.H, self.W, self.patch_H, self.patch_W = H, W, patch_H, patch_W
+        self._lie_batch = lie_batch
+        self._packed = None
+        self._packed_version = None
+        self.last_flat_grad = None
+
+    def lie_batch(self, B):
+        return self._lie_batch if self._lie_batch > 0 else B
+
+    def grid_geo(self, B, Hm):
+        return grid_geometry(B, self.H, self.W, self.patch_H, self.patch_W, Hm)
+
+    def packed_for(self, params):
+        """Pack the fp32 master weights into the MFMA operand layouts when they changed (tracked by
+        the parameters' in-place version counters, so every optimizer step triggers a re-pack)."""
+        ver = (PARAM_GENERATION[0],) + tuple((p.data_ptr(), p._version) for p in params)
+        if self._packed is not None and ver == self._packed_version:
+            return self._packed
+        dev = params[0].device
+        flat = flat_view(params)
+        if flat is None:
+            flat = torch.cat([p.detach().reshape(-1) for p in params])
+        _f32(flat, "mlp parameters")
+        if self._packed is None or self._packed.device != dev:
+            self._packed = torch.empty(self.net.packed_bytes, dtype=torch.uint8, device=dev)
+        self.net.pack(flat, self._packed)
+        self._packed_version = ver
+        return self._packed
+
+
+def flat_view(tensors):
+    """If `tensors` are consecutive views of one contiguous fp32 storage, return the flat 1-D view
+    covering them (no copy), else None."""
+    if not tensors:
+        return None
+    t0 = tensors[0]
+    st = t0.untyped_storage()
+    off = t0.storage_offset()
+    total = 0
+    for t in tensors:
+        if t.untyped_storage().data_ptr() != st.data_ptr() or not t.is_contiguous() or t.storage_offset() != off + total:
+            return None
+        total += t.numel()
+    return torch.empty(0, dtype=t0.dtype, device=t0.device).set_(st, off, (total,), (1,))
+
+
+def render_train(warp_weight, progress, engine, params, b0=0, b1=None):
+    b1 = warp_weight.shape[0] if b1 is None else b1
+    return _PlanarRenderFunction.apply(warp_weight, progress, engine, b0, b1, *params)
+
+
+def mlp_forward(coords, progress, engine, params):
+    return _MLPFunction.apply(coords, progress, engine, *params)
+
+
+# ====================================================================== loss
+
+class _MaskedMSE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, gt, mask, denom_override):
+        pred, gt = _f32(pred, "pred"), _f32(gt, "labels")
+        mask = None if mask is None else _f32(mask, "masks")
+        B, Np = pred.shape[0], pred.shape[1]
+        out = torch.empty(3, device=pred.device, dtype=torch.float32)
+        ws = _BUFS.get("mse_ws", lib().marf_mse_workspace_bytes(), pred.device)
+        _check(lib().marf_masked_mse(_ptr(pred), _ptr(gt), _ptr(mask), B, Np, _ptr(denom_override), _ptr(out),
+                                     _ptr(ws), _stream(pred)))
+        ctx.save_for_backward(pred, gt, mask, out)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, gout):
+        pred, gt, mask, out = ctx.saved_tensors
+        gout = _f32(gout.reshape(1), "grad")
+        d = torch.empty_like(pred)
+        _check(lib().marf_masked_mse_backward(_ptr(pred), _ptr(gt), _ptr(mask), pred.shape[0], pred.shape[1],
+                                              _ptr(out[1:2]), _ptr(gout), _ptr(d), _stream(pred)))
+        return d, None, None, None
+
+
+def masked_mse(pred_bn3, gt_b3n, mask_b1n=None, denom_override=None):
+    """Graph.mse_loss (model/planar.py:382-391) on the MLP's [B, N, 3] output layout."""
+    return _MaskedMSE.apply(pred_bn3, gt_b3n, mask_b1n, denom_override)
+
+
+def mse_stats(pred_bn3, gt_b3n, mask_b1n=None):
+    """(loss, denom, local 3*sum(mask)) without autograd."""
+    pred, gt = _f32(pred_bn3, "pred"), _f32(gt_b3n, "labels")
+    mask = None if mask_b1n is None else _f32(mask_b1n, "masks")
+    out = torch.empty(3, device=pred.device, dtype=torch.float32)
+    ws = _BUFS.get("mse_ws", lib().marf_mse_workspace_bytes(), pred.device)
+    _check(lib().marf_masked_mse(_ptr(pred), _ptr(gt), _ptr(mask), pred.shape[0], pred.shape[1], None, _ptr(out),
+                                 _ptr(ws), _stream(pred)))
+    return out
+
+
+# ====================================================================== Adam
+
+def adam_step(p, g, m, v, lr, beta1, beta2, eps, step, grad_scale=None):
+    _check(lib().marf_adam_step(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), float(lr), float(beta1), float(beta2),
+                                float(eps), int(step), _ptr(grad_scale), _stream(p)))
+
+
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam (model/planar.py:98-99) with the update in one HIP kernel per contiguous
+    parameter segment.  Same constructor, param groups, state keys (step, exp_avg, exp_avg_sq).
+    Parameters with grad None are skipped, as in torch."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False, **kw):
+        if weight_decay != 0 or amsgrad:
+            raise ValueError("marf Adam: weight_decay / amsgrad are not used by the planar model")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        self._flat_state = {}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            b1, b2 = group["betas"]
+            # one launch per run of consecutive views (the MLP parameters share one flat buffer)
+            runs, cur = [], [ps[0]]
+            for p in ps[1:]:
+                if flat_view(cur + [p]) is not None and flat_view([q.grad for q in cur + [p]]) is not None:
+                    cur.append(p)
+                else:
+                    runs.append(cur)
+                    cur = [p]
+            runs.append(cur)
+            for run in runs:
+                for p in run:
+                    st = self.state[p]
+                    if not st:
+                        st["step"] = 0
+                for p in run:
+                    self.state[p]["step"] += 1
+                step = self.state[run[0]]["step"]
+                if len(run) > 1 and all(self.state[p]["step"] == step for p in run):
+                    pf = flat_view(run)
+                    gf = flat_view([p.grad for p in run])
+                    key = tuple(id(p) for p in run)
+                    if key not in self._flat_state:
+                        m = torch.zeros_like(pf)
+                        v = torch.zeros_like(pf)
+                        self._flat_state[key] = (m, v)
+                        for p, mm, vv in zip(run, _split_grads(m, [q.shape for q in run]),
+                                             _split_grads(v, [q.shape for q in run])):
+                            self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"] = mm, vv
+                    m, v = self._flat_state[key]
+                    adam_step(pf, gf.contiguous(), m, v, group["lr"], b1, b2, group["eps"], step)
+                else:
+                    for p in run:
+                        st = self.state[p]
+                        if "exp_avg" not in st:
+                            st["exp_avg"] = torch.zeros_like(p)
+                            st["exp_avg_sq"] = torch.zeros_like(p)
+                        adam_step(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], group["lr"], b1, b2,
+                                  group["eps"], st["step"])
+        PARAM_GENERATION[0] += 1
+        return loss

@@ -323,12 +323,20 @@ void oracle_pixel_grid(int H, int W, int ph, int pw, int crop, float* xy) {
     }
 }
 
-/* warp.py:74-78 for one point: X = H [x y 1]^T as torch-CPU's bmm computes it
- * (acc = x*H0; acc = fma(y, H1, acc); acc = acc + H2), then X[:2]/(X[2]+1e-8). */
+/* warp.py:74-78 for one point: X = H [x y 1]^T as torch-CPU's bmm computes it, then
+ * X[:2]/(X[2]+1e-8).  Point sets with 3*n*3 >= 400 take torch's BLAS path
+ * (acc = x*H0; acc = fma(y, H1, acc); acc = acc + H2); smaller ones its small-matrix kernel
+ * (separate multiply and add). */
+static int g_bmm_small = 0;
 static void warp_point(const float* Hm, float x, float y, float* u, float* v, float* X) {
     for (int r = 0; r < 3; ++r) {
         float acc = x * Hm[3 * r + 0];
-        acc = fmaf(y, Hm[3 * r + 1], acc);
+        if (g_bmm_small) {
+            float p = y * Hm[3 * r + 1];
+            acc = acc + p;
+        } else {
+            acc = fmaf(y, Hm[3 * r + 1], acc);
+        }
         acc = acc + Hm[3 * r + 2];
         X[r] = acc;
     }
@@ -339,6 +347,7 @@ static void warp_point(const float* Hm, float x, float y, float* u, float* v, fl
 
 /* xy: [B][n][2] input points; Hm: [B][9]; uv: [B][n][2] output. */
 void oracle_warp_points(const float* xy, const float* Hm, float* uv, int B, int n) {
+    g_bmm_small = 9 * n < 400;
     for (int b = 0; b < B; ++b)
         for (int i = 0; i < n; ++i) {
             float X[3];
@@ -398,6 +407,7 @@ void oracle_posenc(const float* coord, int n, int L, const float* w, float* feat
 void oracle_prologue_backward(const float* xy, const float* Hm, const float* dfeat, int n, int L,
                               const float* w, double* dH, float* duv) {
     const float pi_f = (float)3.141592653589793;
+    g_bmm_small = 9 * n < 400;
     int D = 2 + 4 * L;
     for (int i = 0; i < n; ++i) {
         float X[3], uv[2];
