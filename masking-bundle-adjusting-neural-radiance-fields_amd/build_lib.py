@@ -15,7 +15,7 @@ LIB = os.path.join(HERE, "lib", "libmarf.so")
 SOURCES = ["marf_lie.hip", "marf_mlp.hip", "marf_wgrad.hip", "marf_misc.hip", "marf_abi.hip", "marf_prof.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          # exact fp32 operation order for the bit-exact prologue (no implicit FMA contraction)
-         "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
+         "-ffp-contract=off", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function"]
 
 
 def _stale():

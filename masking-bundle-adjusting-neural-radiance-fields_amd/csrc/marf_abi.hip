@@ -303,6 +303,7 @@ static void plan_saved(const marf_net* n, long long S, SavedPlan& p) {
 struct WsPlan {
     size_t dz[MARF_MAX_LAYERS], glast, dH, part, bpart, total;
     int chunk, n_chunks, n_tiles;
+    int chunk_last, n_chunks_last;  // finer split for the bandwidth-bound last-layer wgrad
 };
 
 static void plan_ws(const marf_net* n, long long S, int n_tiles, WsPlan& p) {
@@ -326,11 +327,16 @@ static void plan_ws(const marf_net* n, long long S, int n_tiles, WsPlan& p) {
         mxo = std::max(mxo, (long long)n->Mp[l] * n->Kp[l]);
         mxm = std::max(mxm, (long long)n->Mp[l]);
     }
-    mxo = std::max(mxo, 3LL * n->Kp[n->n_layers - 1]);
+    long long cl = rup((S + 1023) / 1024, 64);
+    if (cl < 64) cl = 64;
+    p.chunk_last = (int)cl;
+    p.n_chunks_last = (int)((S + cl - 1) / cl);
+    long long part_elems = std::max((long long)p.n_chunks * mxo, (long long)p.n_chunks_last * 3 * n->Kp[n->n_layers - 1]);
+    long long bpart_elems = std::max((long long)p.n_chunks * mxm, (long long)p.n_chunks_last * 3);
     p.part = off;
-    off += rup((long long)p.n_chunks * mxo * 4, 256);
+    off += rup(part_elems * 4, 256);
     p.bpart = off;
-    off += rup((long long)p.n_chunks * std::max(mxm, 3LL) * 4, 256);
+    off += rup(bpart_elems * 4, 256);
     p.total = off;
 }
 
@@ -442,11 +448,11 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
         const int l = nl - 1;
         {
             MarfProfScope ps("wgrad_last", s);
-            HIPCHK(marf_launch_wgrad_last(net->dtype, a.glast, sv + sp.feat[l], a.S, net->Kp[l], net->Kp[l], wp.chunk,
-                                          wp.n_chunks, part, bpart, s),
+            HIPCHK(marf_launch_wgrad_last(net->dtype, a.glast, sv + sp.feat[l], a.S, net->Kp[l], net->Kp[l],
+                                          wp.chunk_last, wp.n_chunks_last, part, bpart, s),
                    "backward wgrad last");
         }
-        HIPCHK(marf_launch_wgrad_reduce(part, bpart, wp.n_chunks, 3, net->Kp[l], 3, net->dims[l],
+        HIPCHK(marf_launch_wgrad_reduce(part, bpart, wp.n_chunks_last, 3, net->Kp[l], 3, net->dims[l],
                                         d_dparams + net->w_off[l], d_dparams + net->b_off[l], s),
                "backward wgrad last reduce");
     }

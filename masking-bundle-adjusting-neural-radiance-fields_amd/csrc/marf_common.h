@@ -27,11 +27,9 @@ typedef unsigned short u16;
 // ------------------------------------------------------------------ bf16 helpers
 
 MARF_DEV u16 f2bf(float x) {
-    // round-to-nearest-even, NaN kept NaN (matches torch's float->bfloat16 conversion)
-    uint32_t u = __float_as_uint(x);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (u16)((u >> 16) | 0x40);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (u16)(u >> 16);
+    // hardware v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN (torch's conversion)
+    __bf16 b = static_cast<__bf16>(x);
+    return __builtin_bit_cast(u16, b);
 }
 MARF_DEV float bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
 

@@ -48,20 +48,27 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
                         const typename P::T* act, int lda, int wave, int lane) {
     const int ko = P::kofs(lane);
     const int rl = lane & 31;
-    const typename P::T* wrow[NA > 0 ? NA : 1];
+    const typename P::T* wrow[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) wrow[i] = W + (size_t)((wave + 4 * i) * 32 + rl) * K + ko;
     const typename P::T* brow = act + (size_t)rl * lda + ko;
+    // weight fragments stream from L2: software-pipelined one k-step ahead of the MFMAs
+    typename P::frag a[NA], an[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) a[i] = P::load_frag(wrow[i]);
     for (int k0 = 0; k0 < K; k0 += P::KS) {
-        typename P::frag a[NA > 0 ? NA : 1];
+        const int kn = k0 + P::KS < K ? k0 + P::KS : k0;
 #pragma unroll
-        for (int i = 0; i < NA; ++i) a[i] = P::load_frag(wrow[i] + k0);
+        for (int i = 0; i < NA; ++i) an[i] = P::load_frag(wrow[i] + kn);
+        typename P::frag b[PT];
 #pragma unroll
-        for (int j = 0; j < PT; ++j) {
-            typename P::frag b = P::load_frag(brow + (size_t)j * 32 * lda + k0);
+        for (int j = 0; j < PT; ++j) b[j] = P::load_frag(brow + (size_t)j * 32 * lda + k0);
 #pragma unroll
-            for (int i = 0; i < NA; ++i) acc[i][j] = P::mma32(a[i], b, acc[i][j]);
-        }
+        for (int j = 0; j < PT; ++j)
+#pragma unroll
+            for (int i = 0; i < NA; ++i) acc[i][j] = P::mma32(a[i], b[j], acc[i][j]);
+#pragma unroll
+        for (int i = 0; i < NA; ++i) a[i] = an[i];
     }
 }
 

@@ -43,8 +43,11 @@ template <class P, int RT, int CT>
 __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
     typedef typename P::T T;
     constexpr int BM = WgGeo<RT, CT>::BM, BN = WgGeo<RT, CT>::BN;
-    constexpr int PADE = sizeof(T) == 2 ? 32 : 1;  // row padding (elements)
+    constexpr int PADE = sizeof(T) == 2 ? 32 : 4;  // row padding (elements), keeps rows 16-B aligned
     constexpr int LDZ = BM + PADE, LDF = BN + PADE;
+    constexpr int VEC = 16 / sizeof(T);          // elements per 16-byte vector
+    constexpr int NVZ = 64 * BM / VEC / 512;     // dz vectors per thread and stage
+    constexpr int NVF = 64 * BN / VEC / 512;     // feat vectors per thread and stage
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* tz = reinterpret_cast<T*>(smem);          // [64][LDZ]
     T* tf = tz + 64 * LDZ;                        // [64][LDF]
@@ -66,39 +69,45 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
         for (int j = 0; j < CT; ++j) acc[i][j] = (f32x16){};
     float bsum = 0.f;
 
-    for (long long s0 = s_begin; s0 < s_end; s0 += 64) {
-        // ---- stage 64 pixel rows of dz (cols m0..m0+BM) and feat (cols k0..k0+BN)
-        __syncthreads();
-        if (sizeof(T) == 2) {
-            for (int e = threadIdx.x; e < 64 * (BM / 8); e += 512) {
-                int r = e / (BM / 8), c = (e % (BM / 8)) * 8;
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (s0 + r < s_end && m0 + c < a.M)
-                    v = *reinterpret_cast<const uint4*>(dz + (s0 + r) * a.ldz + m0 + c);
-                *reinterpret_cast<uint4*>(tz + r * LDZ + c) = v;
-            }
-            for (int e = threadIdx.x; e < 64 * (BN / 8); e += 512) {
-                int r = e / (BN / 8), c = (e % (BN / 8)) * 8;
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (s0 + r < s_end && k0 + c < a.K)
-                    v = *reinterpret_cast<const uint4*>(ft + (s0 + r) * a.ldf + k0 + c);
-                *reinterpret_cast<uint4*>(tf + r * LDF + c) = v;
-            }
-        } else {
-            for (int e = threadIdx.x; e < 64 * BM; e += 512) {
-                int r = e / BM, c = e % BM;
-                T v = 0;
-                if (s0 + r < s_end && m0 + c < a.M) v = dz[(s0 + r) * a.ldz + m0 + c];
-                tz[r * LDZ + c] = v;
-            }
-            for (int e = threadIdx.x; e < 64 * BN; e += 512) {
-                int r = e / BN, c = e % BN;
-                T v = 0;
-                if (s0 + r < s_end && k0 + c < a.K) v = ft[(s0 + r) * a.ldf + k0 + c];
-                tf[r * LDF + c] = v;
-            }
+    // stage s0 -> registers (16-byte vectors, zero outside the chunk / the matrix)
+    uint4 rz[NVZ], rf[NVF];
+    auto load_stage = [&](long long s0) {
+#pragma unroll
+        for (int q = 0; q < NVZ; ++q) {
+            const int e = threadIdx.x + 512 * q;
+            const int r = e / (BM / VEC), c = (e % (BM / VEC)) * VEC;
+            rz[q] = make_uint4(0, 0, 0, 0);
+            if (s0 + r < s_end && m0 + c < a.M) rz[q] = *reinterpret_cast<const uint4*>(dz + (s0 + r) * a.ldz + m0 + c);
         }
+#pragma unroll
+        for (int q = 0; q < NVF; ++q) {
+            const int e = threadIdx.x + 512 * q;
+            const int r = e / (BN / VEC), c = (e % (BN / VEC)) * VEC;
+            rf[q] = make_uint4(0, 0, 0, 0);
+            if (s0 + r < s_end && k0 + c < a.K) rf[q] = *reinterpret_cast<const uint4*>(ft + (s0 + r) * a.ldf + k0 + c);
+        }
+    };
+    auto store_stage = [&]() {
+#pragma unroll
+        for (int q = 0; q < NVZ; ++q) {
+            const int e = threadIdx.x + 512 * q;
+            const int r = e / (BM / VEC), c = (e % (BM / VEC)) * VEC;
+            *reinterpret_cast<uint4*>(tz + r * LDZ + c) = rz[q];
+        }
+#pragma unroll
+        for (int q = 0; q < NVF; ++q) {
+            const int e = threadIdx.x + 512 * q;
+            const int r = e / (BN / VEC), c = (e % (BN / VEC)) * VEC;
+            *reinterpret_cast<uint4*>(tf + r * LDF + c) = rf[q];
+        }
+    };
+
+    if (s_begin < s_end) load_stage(s_begin);
+    for (long long s0 = s_begin; s0 < s_end; s0 += 64) {
+        __syncthreads();  // previous stage fully consumed
+        store_stage();
         __syncthreads();
+        if (s0 + 64 < s_end) load_stage(s0 + 64);  // next stage in flight behind the MFMAs
 
         if (do_bias) {
             // db partial: thread t sums column t%BM over rows t/BM, t/BM + 512/BM, ...
@@ -178,42 +187,72 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
     }
 }
 
-// Last layer (3 outputs): dW[c][k] = sum_px g[px][c] feat[px][k] on the VALU (K <= 1024).
+// Last layer (3 outputs): dW[c][k] = sum_px g[px][c] feat[px][k], db[c] = sum_px g[px][c].
+// Bandwidth-bound (reads feat_{n-1} once): each thread owns VEC consecutive features (one 16-byte
+// load per pixel row) and a pixel lane; a wave covers whole rows so every load instruction is
+// contiguous.  Pixel lanes are summed through LDS at the end (fixed order).
 template <class P>
 __global__ __launch_bounds__(256) void k_wgrad_last(const float* __restrict__ glast, const void* feat_v, long long S,
                                                     int ldf, int K, int chunk, float* partial, float* bpartial) {
     typedef typename P::T T;
+    constexpr int VEC = 16 / sizeof(T);
+    __shared__ float red[3072];
+    __shared__ float redb[256][3];
     const T* feat = reinterpret_cast<const T*>(feat_v);
+    const int ngrp = K / VEC;               // feature groups (K is a multiple of 32)
+    const int lanes = 256 / ngrp;           // pixel lanes (>= 1 for K <= 256*VEC)
+    const int t = threadIdx.x;
+    const int fg = t % ngrp, pl = t / ngrp;
+    const bool active = pl < lanes;
     const long long s_begin = (long long)blockIdx.x * chunk;
     const long long s_end = min(s_begin + chunk, S);
-    float acc[4][3];
-    for (int j = 0; j < 4; ++j)
-        for (int c = 0; c < 3; ++c) acc[j][c] = 0.f;
-    float bs[3] = {0.f, 0.f, 0.f};
-    for (long long s = s_begin; s < s_end; ++s) {
-        float4 g = *reinterpret_cast<const float4*>(glast + s * 4);
+    float acc[VEC][3];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            int k = threadIdx.x + 256 * j;
-            if (k < K) {
-                float f = P::tof(feat[s * ldf + k]);
-                acc[j][0] += g.x * f;
-                acc[j][1] += g.y * f;
-                acc[j][2] += g.z * f;
+    for (int v = 0; v < VEC; ++v) acc[v][0] = acc[v][1] = acc[v][2] = 0.f;
+    float b0 = 0.f, b1 = 0.f, b2 = 0.f;
+    if (active) {
+        long long s = s_begin + pl;
+#pragma unroll 4
+        for (; s < s_end; s += lanes) {
+            const float4 g = *reinterpret_cast<const float4*>(glast + s * 4);
+            const uint4 raw = *reinterpret_cast<const uint4*>(feat + s * ldf + fg * VEC);
+            const T* f = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) {
+                const float x = P::tof(f[v]);
+                acc[v][0] += g.x * x;
+                acc[v][1] += g.y * x;
+                acc[v][2] += g.z * x;
             }
+            b0 += g.x;
+            b1 += g.y;
+            b2 += g.z;
         }
-        bs[0] += g.x;
-        bs[1] += g.y;
-        bs[2] += g.z;
     }
+    // pixel-lane reduction through LDS, lanes added in a fixed order: red[k][c], K*3 <= 3072
     float* out = partial + (size_t)blockIdx.x * 3 * K;
-    for (int j = 0; j < 4; ++j) {
-        int k = threadIdx.x + 256 * j;
-        if (k < K)
-            for (int c = 0; c < 3; ++c) out[c * K + k] = acc[j][c];
+    for (int lane_id = 0; lane_id < lanes; ++lane_id) {
+        if (active && pl == lane_id) {
+#pragma unroll
+            for (int v = 0; v < VEC; ++v)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    float* r = &red[(fg * VEC + v) * 3 + c];
+                    *r = lane_id == 0 ? acc[v][c] : *r + acc[v][c];
+                }
+        }
+        __syncthreads();
     }
-    if (threadIdx.x == 0)
-        for (int c = 0; c < 3; ++c) bpartial[(size_t)blockIdx.x * 3 + c] = bs[c];
+    for (int e = t; e < K * 3; e += 256) out[(e % 3) * K + e / 3] = red[e];
+    redb[t][0] = (active && fg == 0) ? b0 : 0.f;
+    redb[t][1] = (active && fg == 0) ? b1 : 0.f;
+    redb[t][2] = (active && fg == 0) ? b2 : 0.f;
+    __syncthreads();
+    if (t < 3) {
+        float sb = 0.f;
+        for (int i = 0; i < 256; ++i) sb += redb[i][t];
+        bpartial[(size_t)blockIdx.x * 3 + t] = sb;
+    }
 }
 
 // Fixed-order sum of the chunk partials into the flat fp32 gradient (nn.Linear layout [M][K],
@@ -245,7 +284,7 @@ template <class P, int RT, int CT>
 static hipError_t launch_wg(const WgArgs& a, int n_chunks, int n_oblk, hipStream_t s) {
     typedef typename P::T T;
     constexpr int BM = WgGeo<RT, CT>::BM, BN = WgGeo<RT, CT>::BN;
-    constexpr int PADE = sizeof(T) == 2 ? 32 : 1;
+    constexpr int PADE = sizeof(T) == 2 ? 32 : 4;
     size_t lds = (size_t)64 * (BM + PADE + BN + PADE) * sizeof(T);
     if (lds < 512 * sizeof(float)) lds = 512 * sizeof(float);
     static bool attr = false;

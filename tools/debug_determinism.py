@@ -37,7 +37,7 @@ for it in range(4):
     snaps.append(dict(ws=marf_hip._BUFS.bufs["planar_ws"].clone(), saved=marf_hip._BUFS.bufs["planar_saved"].clone(),
                       dh=graph.warp_param.weight.grad.clone(), rgb=v.rgb_prediction.detach().clone()))
 S = B * 65536
-Kp = [96 if L == 16 else 64, 256, 256, 256, 256]
+Kp = [(2 + 4 * L + 31) // 32 * 32, 256, 256, 256, 256]
 esz = 2 if prec == "bf16" else 4
 off = 0
 regions = {}
@@ -61,3 +61,7 @@ for i in range(1, 4):
         pb = b["ws"][s0:s1].view(torch.float32).view(-1, 9)
         rows = (pa != pb).any(1).nonzero().flatten()
         print("   differing dH tiles:", rows[:20].tolist(), "count", rows.numel())
+    if name == "dH" and rows.numel():
+        r = int(rows[0])
+        print("   tile", r, "run0", pa[r].tolist())
+        print("   tile", r, "runi", pb[r].tolist())
