@@ -375,7 +375,7 @@ int marf_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* 
         SavedPlan p;
         plan_saved(net, a.S, p);
         for (int l = 0; l < net->n_layers; ++l) a.feat[l] = (char*)d_saved + p.feat[l];
-        for (int l = 1; l < net->n_layers; ++l) a.mask[l] = (uint32_t*)((char*)d_saved + p.mask[l]);
+        for (int l = 1; l < net->n_layers; ++l) a.mask[l] = (uint64_t*)((char*)d_saved + p.mask[l]);
     }
     int n_tiles = (int)(a.S / net->TP);
     {
@@ -412,7 +412,7 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
     char* ws = (char*)d_workspace;
     const char* sv = (const char*)d_saved;
     for (int l = 1; l < net->n_layers; ++l) {
-        a.mask[l] = (const uint32_t*)(sv + sp.mask[l]);
+        a.mask[l] = (const uint64_t*)(sv + sp.mask[l]);
         a.dz[l] = ws + wp.dz[l];
     }
     a.glast = (float*)(ws + wp.glast);

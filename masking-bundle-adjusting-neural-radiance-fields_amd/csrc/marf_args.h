@@ -16,7 +16,7 @@ struct FwdArgs {
     C2fDev c2f;
     float* rgb;                       // [B][Np][3]
     void* feat[MARF_MAX_LAYERS];      // saved layer inputs [S][Kp_l] (nullptr: do not save)
-    uint32_t* mask[MARF_MAX_LAYERS];  // relu masks of feat_l (l >= 1) [Kp_l/32][S]
+    uint64_t* mask[MARF_MAX_LAYERS];  // relu masks of feat_l (l >= 1), wave-ballot layout (marf_common.h)
     long long S;
     int lda;                          // LDS row stride (elements)
 };
@@ -27,7 +27,7 @@ struct BwdArgs {
     C2fDev c2f;
     const float* rgb;                       // [B][Np][3] forward output
     const float* d_rgb;                     // [B][Np][3]
-    const uint32_t* mask[MARF_MAX_LAYERS];  // from forward
+    const uint64_t* mask[MARF_MAX_LAYERS];  // from forward
     void* dz[MARF_MAX_LAYERS];              // out: dz_l (l >= 1) [S][Kp_l] (grad of layer l-1 pre-act)
     float* glast;                           // out: [S][4] grad of the last layer pre-activation
     float* dH_partial;                      // out (geo mode 0): [n_tiles][9]

@@ -5,7 +5,9 @@
 //     up to MARF_TILE_PAD); slots with p >= Np are padding (never written to user outputs, zero
 //     gradient).
 //   * saved activations  feat_l : [S][Kp_l]  (storage type T, pixel-major rows)
-//   * relu masks         mask_l : [Kp_l/32][S] uint32, bit j of word t <-> feature 32t+j > 0
+//   * relu masks         mask_l : uint64 [S/32][Kp_l/32][16]: for pixel tile p (32 slots), row tile t and
+//                        accumulator register r, bit `lane` = (feature 32t + acc_row(lane, r) of
+//                        slot 32p + (lane & 31)) > 0 -- the wave ballot of that register.
 //   * packed weights     Wf_l   : [Mp_l][Kp_l] T (forward A operand, nn.Linear row layout, zero pad)
 //                        Wt_l   : [Kp_l][Mt_l] T (transposed, backward A operand)
 //   * MFMA 32x32 accumulator map (both dtypes): lane l, reg r -> col = l&31,
@@ -21,6 +23,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
 #define MARF_DEV __device__ __forceinline__
 
@@ -176,6 +179,32 @@ MARF_DEV float c2f_weight(float progress, float start, float end_minus_start, in
 MARF_DEV float posenc_arg(float c, int k) {
     const float pi_f = 3.14159265358979323846f;
     return ldexpf(c * pi_f, k);
+}
+
+// sin / cos of the posenc argument x = 2^k * fl(c * pi_f32).
+//   exact (fp32 path): ocml sincosf of the fp32 argument, as torch evaluates it.
+//   fast (bf16 path, whose features are rounded to bf16 = 2^-9 relative anyway): reduce x to
+//   revolutions f = frac(x / 2pi) with a double-float product (|error| < 2^-40 rev for k <= 20),
+//   then the hardware v_sin_f32 / v_cos_f32, which take revolutions.  ~10 VALU instead of ~100.
+template <bool kFast>
+MARF_DEV void band_sincos(float c, int k, float& s, float& co) {
+    const float pi_f = 3.14159265358979323846f;
+    const float y = c * pi_f;
+    if constexpr (kFast) {
+        const float r_hi = 0.159154936671257019f;    // fl(1 / 2pi)
+        const float r_lo = 6.42063831672591501e-09f;  // 1/2pi - r_hi
+        float th = y * r_hi;
+        float tl = __fmaf_rn(y, r_hi, -th);          // exact product error
+        tl = __fmaf_rn(y, r_lo, tl);
+        th = ldexpf(th, k);
+        tl = ldexpf(tl, k);
+        float f = th - rintf(th);                    // exact
+        f = f + tl;
+        s = __builtin_amdgcn_sinf(f);
+        co = __builtin_amdgcn_cosf(f);
+    } else {
+        sincosf(ldexpf(y, k), &s, &co);
+    }
 }
 
 MARF_DEV float wave_sum(float v) {

@@ -48,19 +48,31 @@ __global__ void k_mse_partial(const float* __restrict__ pred, const float* __res
 
 // loss = f32(num) / (f32(sum m) * 3)   (model/planar.py:390); out[0] = loss, out[1] = denominator.
 // denom_override (device scalar, optional): the global 3*sum(mask) when the patches are sharded over
-// ranks (each rank then returns its share of the global loss).
-__global__ void k_mse_final(const double* __restrict__ part, int nblk, float* __restrict__ out,
-                            const float* __restrict__ denom_override) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// ranks (each rank then returns its share of the global loss).  Fixed-order tree in fp64.
+__global__ __launch_bounds__(256) void k_mse_final(const double* __restrict__ part, int nblk, float* __restrict__ out,
+                                                   const float* __restrict__ denom_override) {
+    __shared__ double rn[256], rm[256];
     double num = 0.0, ms = 0.0;
-    for (int i = 0; i < nblk; ++i) {
+    for (int i = threadIdx.x; i < nblk; i += 256) {
         num += part[2 * i];
         ms += part[2 * i + 1];
     }
-    float denom = denom_override ? denom_override[0] : (float)ms * 3.0f;
-    out[0] = (float)num / denom;
-    out[1] = denom;
-    out[2] = (float)ms * 3.0f;
+    rn[threadIdx.x] = num;
+    rm[threadIdx.x] = ms;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            rn[threadIdx.x] += rn[threadIdx.x + o];
+            rm[threadIdx.x] += rm[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        float denom = denom_override ? denom_override[0] : (float)rm[0] * 3.0f;
+        out[0] = (float)rn[0] / denom;
+        out[1] = denom;
+        out[2] = (float)rm[0] * 3.0f;
+    }
 }
 
 // d pred = ((gout / denom) * (2 * (pred - gt) * m)) * m   (autograd of model/planar.py:388-390)
@@ -189,7 +201,7 @@ hipError_t marf_launch_mse(const float* pred, const float* gt, const float* mask
     int nb = grid_for((long long)B * Np);
     if (nb > 1024) nb = 1024;
     hipLaunchKernelGGL(k_mse_partial, dim3(nb), dim3(256), 0, s, pred, gt, mask, B, Np, part);
-    hipLaunchKernelGGL(k_mse_final, dim3(1), dim3(64), 0, s, part, nb, out, denom_override);
+    hipLaunchKernelGGL(k_mse_final, dim3(1), dim3(256), 0, s, part, nb, out, denom_override);
     return hipGetLastError();
 }
 

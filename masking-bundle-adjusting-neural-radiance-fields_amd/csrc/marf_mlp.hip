@@ -25,13 +25,21 @@ namespace marf {
 template <class P>
 MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int cols, typename P::T* dst, int ldd) {
     // LDS [rows][lda] -> global [rows][ldd], first `cols` columns. bf16: 16-byte chunks.
+    // The (row, chunk) walk is incremental: one division per call, none per element.
     typedef typename P::T T;
     if (sizeof(T) == 2) {
         const int nch = cols / 8;
-        for (int e = threadIdx.x; e < rows * nch; e += blockDim.x) {
-            int r = e / nch, c = e - r * nch;
+        const int step = blockDim.x, dr = step / nch, dc = step - dr * nch;
+        int r = threadIdx.x / nch, c = threadIdx.x - r * nch;
+        for (; r < rows;) {
             uint4 v = *reinterpret_cast<const uint4*>(act + (size_t)r * lda + 8 * c);
             *reinterpret_cast<uint4*>(dst + (size_t)r * ldd + 8 * c) = v;
+            r += dr;
+            c += dc;
+            if (c >= nch) {
+                c -= nch;
+                ++r;
+            }
         }
     } else {
         for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
@@ -41,44 +49,127 @@ MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int col
     }
 }
 
-// acc[i][PT] = W[rows (wave + 4 i)*32 .., k] . act[px, k]^T over k < K for the NA row tiles this
-// wave owns (i < NA).  Branch-free body; NA is dispatched once per layer (wave-uniform).
+// acc[i][PT] += W[rows (wave + 4 i)*32 .., k] . act[px, k]^T over k < K for the NA row tiles this
+// wave owns (i < NA).  NA is dispatched once per layer (wave-uniform), so the body is branch-free.
+//
+// Schedule: the weight fragments stream from L2 through a static 4-deep register ring (slot u is
+// reloaded for k-step k+4 right after its MFMAs issue: three k-steps of latency cover, no register
+// moves), the activation fragments of step k+1 are read from LDS while step k's MFMAs run (two
+// statically named buffers).  Loads past the last k-step are clamped to it (harmless L2 hits).
 template <class P, int NA, int RT, int PT>
 MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__ W, int K,
                         const typename P::T* act, int lda, int wave, int lane) {
+    typedef typename P::frag F;
     const int ko = P::kofs(lane);
     const int rl = lane & 31;
+    const int nk = K / P::KS;
     const typename P::T* wrow[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) wrow[i] = W + (size_t)((wave + 4 * i) * 32 + rl) * K + ko;
     const typename P::T* brow = act + (size_t)rl * lda + ko;
-    // weight fragments stream from L2: software-pipelined one k-step ahead of the MFMAs
-    typename P::frag a[NA], an[NA];
+    auto ldA = [&](F (&dst)[NA], int k) {
+        const int kc = (k < nk ? k : nk - 1) * P::KS;
 #pragma unroll
-    for (int i = 0; i < NA; ++i) a[i] = P::load_frag(wrow[i]);
-    for (int k0 = 0; k0 < K; k0 += P::KS) {
-        const int kn = k0 + P::KS < K ? k0 + P::KS : k0;
+        for (int i = 0; i < NA; ++i) dst[i] = P::load_frag(wrow[i] + kc);
+    };
+    auto ldB = [&](F (&dst)[PT], int k) {
+        const int kc = (k < nk ? k : nk - 1) * P::KS;
 #pragma unroll
-        for (int i = 0; i < NA; ++i) an[i] = P::load_frag(wrow[i] + kn);
-        typename P::frag b[PT];
-#pragma unroll
-        for (int j = 0; j < PT; ++j) b[j] = P::load_frag(brow + (size_t)j * 32 * lda + k0);
+        for (int j = 0; j < PT; ++j) dst[j] = P::load_frag(brow + (size_t)j * 32 * lda + kc);
+    };
+    auto mma = [&](const F (&a)[NA], const F (&b)[PT]) {
 #pragma unroll
         for (int j = 0; j < PT; ++j)
 #pragma unroll
             for (int i = 0; i < NA; ++i) acc[i][j] = P::mma32(a[i], b[j], acc[i][j]);
-#pragma unroll
-        for (int i = 0; i < NA; ++i) a[i] = an[i];
+    };
+    F A0[NA], A1[NA], A2[NA], A3[NA], B0[PT], B1[PT];
+    if constexpr (sizeof(F) * NA > 32) {
+        // wide row blocks (bf16, NA > 2): a 2-deep ring keeps the kernel inside 256 VGPRs
+        ldA(A0, 0);
+        ldA(A1, 1);
+        ldB(B0, 0);
+        int k = 0;
+        for (; k + 2 <= nk; k += 2) {
+            ldB(B1, k + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(A0, B0);
+            __builtin_amdgcn_sched_barrier(0);
+            ldA(A0, k + 2);
+            ldB(B0, k + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(A1, B1);
+            __builtin_amdgcn_sched_barrier(0);
+            ldA(A1, k + 3);
+        }
+        if (k < nk) mma(A0, B0);
+        return;
+    }
+    ldA(A0, 0);
+    ldA(A1, 1);
+    ldA(A2, 2);
+    ldA(A3, 3);
+    ldB(B0, 0);
+    int k = 0;
+    // sched_barrier pins the issue order: left alone, the scheduler sinks every weight load to
+    // the loop end (one MFMA of latency cover) and folds the two B buffers into one.
+    for (; k + 4 <= nk; k += 4) {
+        ldB(B1, k + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A0, B0);
+        __builtin_amdgcn_sched_barrier(0);
+        ldA(A0, k + 4);
+        ldB(B0, k + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A1, B1);
+        __builtin_amdgcn_sched_barrier(0);
+        ldA(A1, k + 5);
+        ldB(B1, k + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A2, B0);
+        __builtin_amdgcn_sched_barrier(0);
+        ldA(A2, k + 6);
+        ldB(B0, k + 4);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A3, B1);
+        __builtin_amdgcn_sched_barrier(0);
+        ldA(A3, k + 7);
+    }
+    // remainder (nk % 4 steps): A0..A2 hold steps k..k+2, B0 holds step k
+    if (k < nk) {
+        ldB(B1, k + 1);
+        mma(A0, B0);
+        if (k + 1 < nk) {
+            ldB(B0, k + 2);
+            mma(A1, B1);
+            if (k + 2 < nk) mma(A2, B0);
+        }
     }
 }
 
+// Accumulators start at the bias of their output row when `bias` is given (so the epilogue does
+// not add it), else at zero.
 template <class P, int RT, int PT>
 MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__ W, int K, int n_rt,
-                        const typename P::T* act, int lda, int wave, int lane) {
+                        const typename P::T* act, int lda, int wave, int lane, const float* bias = nullptr) {
 #pragma unroll
-    for (int i = 0; i < RT; ++i)
+    for (int i = 0; i < RT; ++i) {
+        f32x16 init = (f32x16){};
+        const int rt = wave + 4 * i;
+        if (bias && rt < n_rt) {
+            const float* bb = bias + rt * 32 + 4 * (lane >> 5);
 #pragma unroll
-        for (int j = 0; j < PT; ++j) acc[i][j] = (f32x16){};
+            for (int q = 0; q < 4; ++q) {
+                const float4 bv = *reinterpret_cast<const float4*>(bb + 8 * q);
+                init[4 * q] = bv.x;
+                init[4 * q + 1] = bv.y;
+                init[4 * q + 2] = bv.z;
+                init[4 * q + 3] = bv.w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PT; ++j) acc[i][j] = init;
+    }
     int na = (n_rt - wave + 3) / 4;
     na = na < 0 ? 0 : (na > RT ? RT : na);
     switch (na) {
@@ -94,9 +185,11 @@ MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
 template <class P>
 MARF_DEV void store4(typename P::T* dst, float x0, float x1, float x2, float x3) {
     if (sizeof(typename P::T) == 2) {
-        uint2 v;
-        v.x = (uint32_t)f2bf(x0) | ((uint32_t)f2bf(x1) << 16);
-        v.y = (uint32_t)f2bf(x2) | ((uint32_t)f2bf(x3) << 16);
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        uint2 v;  // one v_cvt_pk_bf16_f32 per pair (RNE)
+        v.x = __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){x0, x1}), bf16x2));
+        v.y = __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){x2, x3}), bf16x2));
         *reinterpret_cast<uint2*>(dst) = v;
     } else {
         float* d = reinterpret_cast<float*>(dst);
@@ -144,23 +237,22 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
         float x, y, u = 0.f, v = 0.f, X[3];
         slot_point(a.geo, b, p0 + i, x, y, u, v, X);
         T* row = act + (size_t)i * lda;
-        const int n_items = 1 + 2 * L;
-        for (int it = part; it < n_items; it += NPART) {
-            if (it == 0) {
-                row[0] = P::cvt(u);
-                row[1] = P::cvt(v);
-            } else {
-                int c = (it - 1) / L, k = (it - 1) - c * L;
-                float s, co;
-                sincosf(posenc_arg(c == 0 ? u : v, k), &s, &co);
-                float w = wsh[k];
-                if (a.c2f.on) {
-                    s = s * w;
-                    co = co * w;
-                }
-                row[2 + c * 2 * L + k] = P::cvt(s);
-                row[2 + c * 2 * L + L + k] = P::cvt(co);
+        if (part == NPART - 1) {
+            row[0] = P::cvt(u);
+            row[1] = P::cvt(v);
+        }
+        // band q = c*L + k of coordinate c: sin at 2 + 2cL + k, cos at 2 + 2cL + L + k
+        for (int q = part; q < 2 * L; q += NPART) {
+            const int c = q >= L, k = q - c * L;
+            float s, co;
+            band_sincos<sizeof(T) == 2>(c ? v : u, k, s, co);
+            if (a.c2f.on) {
+                const float w = wsh[k];
+                s = s * w;
+                co = co * w;
             }
+            row[2 + q + c * L] = P::cvt(s);
+            row[2 + q + c * L + L] = P::cvt(co);
         }
         for (int f = net.D + part; f < net.Kp[0]; f += NPART) row[f] = P::cvt(0.f);
     }
@@ -172,40 +264,37 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
     for (int l = 0; l < nl - 1; ++l) {
         const int K = net.Kp[l], M = net.Mp[l], n_rt = M / 32;
         f32x16 acc[RT][PT];
-        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane);
+        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l]);
         __syncthreads();  // every wave has consumed the layer input
-        uint32_t* mk = a.mask[l + 1];
+        uint64_t* mk = a.mask[l + 1];
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
             const int rt = wave + 4 * i;
             if (rt >= n_rt) continue;
             const int rbase = rt * 32 + 4 * (lane >> 5);
-            float bias[16];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float4 bv = *reinterpret_cast<const float4*>(net.bias[l] + rbase + 8 * q);
-                bias[4 * q] = bv.x;
-                bias[4 * q + 1] = bv.y;
-                bias[4 * q + 2] = bv.z;
-                bias[4 * q + 3] = bv.w;
-            }
 #pragma unroll
             for (int j = 0; j < PT; ++j) {
                 const int px = j * 32 + (lane & 31);
-                uint32_t bits = 0;
                 float o[16];
+                uint64_t bal[16];  // the v_cmp results themselves (SGPR pairs)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    float z = acc[i][j][r] + bias[r];
-                    bool pos = z > 0.f;
+                    const float z = acc[i][j][r];
+                    const bool pos = z > 0.f;
                     o[r] = pos ? z : 0.f;
-                    bits |= (uint32_t)pos << acc_row(lane, r);
+                    bal[r] = __ballot(pos);
                 }
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     store4<P>(act + (size_t)px * lda + rbase + 8 * q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-                bits |= __shfl_xor(bits, 32, 64);
-                if (mk && lane < 32) mk[(long long)rt * a.S + slot0 + px] = bits;
+                if (mk) {
+                    // 128 contiguous bytes per (pixel tile, row tile), written from SGPRs through
+                    // the scalar cache (no VALU); flushed to L2 by s_dcache_wb before the wave ends
+                    uint64_t* mrow = mk + (((slot0 >> 5) + j) * n_rt + rt) * 16;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        asm volatile("s_store_dwordx2 %0, %1, %2" : : "s"(bal[r]), "s"(mrow), "n"(8 * r) : "memory");
+                }
             }
         }
         __syncthreads();
@@ -248,6 +337,8 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
             }
         }
     }
+    // write the scalar-cache mask lines back to L2 (the backward kernel reads them)
+    asm volatile("s_dcache_wb\n\ts_waitcnt lgkmcnt(0)" : : : "memory");
 }
 
 // ======================================================================== backward
@@ -300,7 +391,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(BwdArgs a) {
         f32x16 acc[RT][PT];
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane);
         __syncthreads();
-        const uint32_t* mk = a.mask[l];
+        const uint64_t* mk = a.mask[l];
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
             const int rt = wave + 4 * i;
@@ -309,10 +400,27 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(BwdArgs a) {
 #pragma unroll
             for (int j = 0; j < PT; ++j) {
                 const int px = j * 32 + (lane & 31);
-                const uint32_t bits = mk[(long long)rt * a.S + slot0 + px];
+                // the 16 wave-uniform lane masks of this tile (one per accumulator register),
+                // fetched with two scalar loads into SGPRs; each element is one v_cndmask
+                const uint64_t* mrow = mk + (((slot0 >> 5) + j) * n_rt + rt) * 16;
+                u32x16 m0, m1;
+                asm volatile(
+                    "s_load_dwordx16 %0, %2, 0x0\n\t"
+                    "s_load_dwordx16 %1, %2, 0x40\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    : "=&s"(m0), "=&s"(m1)
+                    : "s"(mrow)
+                    : "memory");
                 float o[16];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) o[r] = ((bits >> acc_row(lane, r)) & 1u) ? acc[i][j][r] : 0.f;
+                for (int r = 0; r < 16; ++r) {
+                    const uint32_t lo = r < 8 ? m0[2 * r] : m1[2 * r - 16];
+                    const uint32_t hi = r < 8 ? m0[2 * r + 1] : m1[2 * r - 15];
+                    const uint64_t ms = ((uint64_t)hi << 32) | lo;
+                    float v;
+                    asm volatile("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(v) : "v"(acc[i][j][r]), "s"(ms));
+                    o[r] = v;
+                }
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     store4<P>(act + (size_t)px * lda + rbase + 8 * q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
@@ -350,25 +458,23 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(BwdArgs a) {
         const bool valid = slot_point(a.geo, b, p0 + i, x, y, u, v, X);
         const float* row = df + (size_t)i * ldf;
         float du = 0.f, dv = 0.f;
-        const int n_items = 1 + 2 * L;
-        for (int it = part; it < n_items; it += NPART) {
-            if (it == 0) {
-                du += row[0];
-                dv += row[1];
-            } else {
-                int c = (it - 1) / L, k = (it - 1) - c * L;
-                float s, co;
-                sincosf(posenc_arg(c == 0 ? u : v, k), &s, &co);
-                float w = wsh[k];
-                float gs = row[2 + c * 2 * L + k], gc = row[2 + c * 2 * L + L + k];
-                if (a.c2f.on) {
-                    gs = gs * w;
-                    gc = gc * w;
-                }
-                float dspec = gs * co - gc * s;
-                float d = dspec * ldexpf(3.14159265358979323846f, k);
-                if (c == 0) du += d; else dv += d;
+        if (part == 0) {
+            du += row[0];
+            dv += row[1];
+        }
+        for (int q = part; q < 2 * L; q += NPART) {
+            const int c = q >= L, k = q - c * L;
+            float s, co;
+            band_sincos<sizeof(T) == 2>(c ? v : u, k, s, co);
+            float gs = row[2 + q + c * L], gc = row[2 + q + c * L + L];
+            if (a.c2f.on) {
+                const float w = wsh[k];
+                gs = gs * w;
+                gc = gc * w;
             }
+            float dspec = gs * co - gc * s;
+            float d = dspec * ldexpf(3.14159265358979323846f, k);
+            if (c == 0) du += d; else dv += d;
         }
         red[part][i][0] = du;
         red[part][i][1] = dv;

@@ -256,23 +256,43 @@ __global__ __launch_bounds__(256) void k_wgrad_last(const float* __restrict__ gl
 }
 
 // Fixed-order sum of the chunk partials into the flat fp32 gradient (nn.Linear layout [M][K],
-// unpadded [Mo][Ko]), then the bias.
-__global__ void k_wgrad_reduce(const float* __restrict__ partial, const float* __restrict__ bpartial, int n_chunks,
-                               int M, int K, int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db) {
+// unpadded [Mo][Ko]), then the bias.  Block = 64 outputs x 4 chunk groups; group g sums chunks
+// [g*n/4, (g+1)*n/4) with independent loads in flight, the 4 group sums are added in order.
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ partial,
+                                                      const float* __restrict__ bpartial, int n_chunks, int M, int K,
+                                                      int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db) {
+    __shared__ float red[4][64];
     const long long n = (long long)Mo * Ko;
-    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n + Mo;
-         e += (long long)gridDim.x * blockDim.x) {
+    const long long e = blockIdx.x * 64LL + (threadIdx.x & 63);
+    const int g = threadIdx.x >> 6;
+    const int c0 = (int)((long long)n_chunks * g / 4), c1 = (int)((long long)n_chunks * (g + 1) / 4);
+    float s = 0.f;
+    if (e < n + Mo) {
+        const float* src;
+        size_t stride;
         if (e < n) {
-            int m = (int)(e / Ko), k = (int)(e % Ko);
-            float s = 0.f;
-            for (int c = 0; c < n_chunks; ++c) s += partial[((size_t)c * M + m) * K + k];
-            dW[e] = s;
+            const int m = (int)(e / Ko), k = (int)(e % Ko);
+            src = partial + (size_t)m * K + k;
+            stride = (size_t)M * K;
         } else {
-            int m = (int)(e - n);
-            float s = 0.f;
-            for (int c = 0; c < n_chunks; ++c) s += bpartial[(size_t)c * M + m];
-            db[m] = s;
+            src = bpartial + (e - n);
+            stride = (size_t)M;
         }
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int c = c0;
+        for (; c + 8 <= c1; c += 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] += src[(size_t)(c + u) * stride];
+        }
+        for (int u = 0; c < c1; ++c, ++u) acc[u] += src[(size_t)c * stride];
+        s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    }
+    red[g][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (g == 0 && e < n + Mo) {
+        const float t = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+        if (e < n) dW[e] = t;
+        else db[e - n] = t;
     }
 }
 
@@ -313,18 +333,21 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
     a.partial = partial;
     a.bpartial = bpartial;
     int cfg;
-    if (M >= 256 && K >= 192) cfg = 0;
-    else if (M >= 256) cfg = 1;
-    else cfg = 2;
-    int BM = cfg == 2 ? 128 : 256, BN = cfg == 0 ? 256 : 64;
+    if (M >= 256 && K >= 192) cfg = 0;       // 256 x 256 (2 x 4 tiles per wave)
+    else if (M >= 256 && K > 64) cfg = 3;    // 256 x 128 (2 x 2): layer 0 at L = 16 reads dz once
+    else if (M >= 256) cfg = 1;              // 256 x 64  (2 x 1)
+    else cfg = 2;                            // 128 x 64  (1 x 1)
+    int BM = cfg == 2 ? 128 : 256, BN = cfg == 0 ? 256 : (cfg == 3 ? 128 : 64);
     int nr = (M + BM - 1) / BM, nc = (K + BN - 1) / BN;
     a.n_oblk_c = nc;
     if (dtype == 1) {
         if (cfg == 0) return launch_wg<PrecBF16, 2, 4>(a, n_chunks, nr * nc, s);
+        if (cfg == 3) return launch_wg<PrecBF16, 2, 2>(a, n_chunks, nr * nc, s);
         if (cfg == 1) return launch_wg<PrecBF16, 2, 1>(a, n_chunks, nr * nc, s);
         return launch_wg<PrecBF16, 1, 1>(a, n_chunks, nr * nc, s);
     }
     if (cfg == 0) return launch_wg<PrecF32, 2, 4>(a, n_chunks, nr * nc, s);
+    if (cfg == 3) return launch_wg<PrecF32, 2, 2>(a, n_chunks, nr * nc, s);
     if (cfg == 1) return launch_wg<PrecF32, 2, 1>(a, n_chunks, nr * nc, s);
     return launch_wg<PrecF32, 1, 1>(a, n_chunks, nr * nc, s);
 }
@@ -343,8 +366,7 @@ hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* fea
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
                                     int Ko, float* dW, float* db, hipStream_t s) {
     long long n = (long long)Mo * Ko + Mo;
-    int blocks = (int)((n + 255) / 256);
-    if (blocks > 4096) blocks = 4096;
+    int blocks = (int)((n + 63) / 64);
     hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, s, partial, bpartial, n_chunks, M, K, Mo, Ko, dW, db);
     return hipGetLastError();
 }

@@ -6,8 +6,11 @@ TAG=${1:-r1}
 OUT=$PWD/gpurun_out
 mkdir -p $OUT
 timeout -k 10 900 python -m pytest tests -m gpu -q -rf -p no:cacheprovider > $OUT/gpu_tests_$TAG.log 2>&1
-echo "pytest exit $?" >> $OUT/gpu_tests_$TAG.log
+RC=$?
+echo "pytest exit $RC" >> $OUT/gpu_tests_$TAG.log
 tail -3 $OUT/gpu_tests_$TAG.log
+# a crash / abort / timeout (not plain test failures) ends the GPU session here
+case $RC in 124|134|137|139) echo "pytest died ($RC): stopping"; exit $RC;; esac
 timeout -k 10 400 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { echo "bench failed $?"; tail -5 $OUT/bench_$TAG.err; exit 1; }
 tail -1 $OUT/bench_$TAG.json | cut -c1-600
 export TMPDIR=/tmp
