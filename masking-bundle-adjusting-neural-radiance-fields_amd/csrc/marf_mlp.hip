@@ -288,12 +288,17 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
                 for (int q = 0; q < 4; ++q)
                     store4<P>(act + (size_t)px * lda + rbase + 8 * q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
                 if (mk) {
-                    // 128 contiguous bytes per (pixel tile, row tile), written from SGPRs through
-                    // the scalar cache (no VALU); flushed to L2 by s_dcache_wb before the wave ends
-                    uint64_t* mrow = mk + (((slot0 >> 5) + j) * n_rt + rt) * 16;
+                    // 128 contiguous bytes per (pixel tile, row tile): the 32 ballot dwords are
+                    // gathered into lanes 0..31 of one VGPR (v_writelane from the SGPR pairs) and
+                    // written with one vector store
+                    uint32_t w = 0;
 #pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        asm volatile("s_store_dwordx2 %0, %1, %2" : : "s"(bal[r]), "s"(mrow), "n"(8 * r) : "memory");
+                    for (int r = 0; r < 16; ++r) {
+                        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"((uint32_t)bal[r]), "n"(2 * r));
+                        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"((uint32_t)(bal[r] >> 32)), "n"(2 * r + 1));
+                    }
+                    uint32_t* mrow = reinterpret_cast<uint32_t*>(mk + (((slot0 >> 5) + j) * n_rt + rt) * 16);
+                    if (lane < 32) mrow[lane] = w;
                 }
             }
         }
@@ -337,8 +342,6 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
             }
         }
     }
-    // write the scalar-cache mask lines back to L2 (the backward kernel reads them)
-    asm volatile("s_dcache_wb\n\ts_waitcnt lgkmcnt(0)" : : : "memory");
 }
 
 // ======================================================================== backward
