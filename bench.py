@@ -207,6 +207,8 @@ def main():
     S = (b1 - b0) * ((h * w + 127) // 128 * 128)
     layer_flops = [2 * a * b for a, b in zip(dims[:-1], dims[1:])]
     kflops = {
+        # fused step: forward + dgrad chain (incl. layer 0, for the warp gradient) + last-layer wgrad
+        "mlp_step": px_local * (2 * sum(layer_flops) + 2 * 3 * dims[-2]),
         "mlp_fwd": S * sum(layer_flops),
         "mlp_bwd_dgrad": S * sum(layer_flops),
         "wgrad_hidden": S * 2 * hidden[0] * hidden[0],

@@ -100,6 +100,21 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
                   const void* d_saved, void* d_workspace, float* d_dparams, float* d_dh, float* d_dcoords,
                   void* stream);
 
+/* ---- Fused training step (grid geometry).  Graph.forward + Graph.mse_loss (model/planar.py:329-336,
+ * 382-391) and the backward of both, computed in one pass per pixel tile because the target and
+ * mask are known at forward time.  marf_step_forward writes rgb [B][Np][3] (may be NULL), the loss
+ * d_loss_out[3] (as marf_masked_mse: loss, denominator, local 3*sum(mask)) and keeps in d_saved
+ * (marf_step_saved_bytes) everything the gradient needs, computed for a unit upstream gradient.
+ * marf_step_backward turns it into d_params (flat, fp32) and d_dh [B][8] for the upstream gradient
+ * *d_gout (device scalar, d loss / d loss_rgb), reading the denominator from d_loss_out[1]. */
+size_t marf_step_saved_bytes(const marf_net* net, const marf_geometry* geo);
+int marf_step_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
+                      const float* d_gt, const float* d_mask, const float* d_denom_override, float* d_rgb,
+                      float* d_loss_out, void* d_saved, void* stream);
+int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void* d_saved, const float* d_h_params,
+                       int lie_batch, const float* d_gout, const float* d_loss_out, float* d_dparams, float* d_dh,
+                       void* stream);
+
 /* ---- Masked MSE (Graph.mse_loss, model/planar.py:382-391).  pred [B][Np][3] (MLP layout),
  * gt [B][3][Np], mask [B][1][Np] or NULL (plain mean).  d_out[3]: loss, denominator used,
  * local 3*sum(mask).  d_denom_override: optional device scalar (global denominator of a patch

@@ -49,7 +49,7 @@ struct marf_net {
     long long wf_off[MARF_MAX_LAYERS], wt_off[MARF_MAX_LAYERS], bias_off[MARF_MAX_LAYERS];
     size_t packed_bytes;
     int TP, lda, Kmax;
-    size_t lds_fwd, lds_bwd;
+    size_t lds_fwd, lds_bwd, lds_step;
     int elem;  // bytes per stored element
 };
 
@@ -212,6 +212,7 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
     size_t df = (size_t)n->TP * (n->Kp[0] + 1) * 4;
     n->lds_fwd = act;
     n->lds_bwd = std::max(act, df);
+    n->lds_step = n->lds_bwd;
     if (n->lds_bwd > 160 * 1024) {
         delete n;
         return fail(MARF_ERR_UNSUPPORTED, "net_create: tile does not fit LDS");
@@ -461,6 +462,152 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
         HIPCHK(marf_launch_reduce_dH(a.dH_partial, a.geo.Np_pad / net->TP, a.geo.B, d_h_params, nullptr, d_dh,
                                      lie_batch > 0 ? lie_batch : a.geo.B, s),
                "backward warp");
+    }
+    return MARF_OK;
+}
+
+// ------------------------------------------------------------------ fused training step
+
+struct StepPlan {
+    size_t feat[MARF_MAX_LAYERS], dz[MARF_MAX_LAYERS], mask[MARF_MAX_LAYERS];
+    size_t wlast, blast, dH, loss, part, bpart, total;
+    int n_tiles, chunk, n_chunks;
+};
+
+static void plan_step(const marf_net* n, long long S, StepPlan& p) {
+    size_t off = 0;
+    const int nl = n->n_layers;
+    p.n_tiles = (int)(S / n->TP);
+    for (int l = 0; l < nl - 1; ++l) {
+        p.feat[l] = off;
+        off += rup((long long)S * n->Kp[l] * n->elem, 256);
+    }
+    p.dz[0] = p.mask[0] = 0;
+    for (int l = 1; l < nl; ++l) {
+        p.dz[l] = off;
+        off += rup((long long)S * n->Kp[l] * n->elem, 256);
+        p.mask[l] = off;
+        off += rup((long long)(n->Kp[l] / 32) * S * 4, 256);
+    }
+    p.wlast = off;
+    off += rup((long long)p.n_tiles * 3 * n->Kp[nl - 1] * 4, 256);
+    p.blast = off;
+    off += rup((long long)p.n_tiles * 3 * 4, 256);
+    p.dH = off;
+    off += rup((long long)p.n_tiles * 9 * 4, 256);
+    p.loss = off;
+    off += rup((long long)p.n_tiles * 2 * 8, 256);
+    long long chunk = rup((S + 255) / 256, 64);
+    if (chunk < 64) chunk = 64;
+    p.chunk = (int)chunk;
+    p.n_chunks = (int)((S + chunk - 1) / chunk);
+    long long mxo = 0, mxm = 0;
+    for (int l = 0; l < nl - 1; ++l) {
+        mxo = std::max(mxo, (long long)n->Mp[l] * n->Kp[l]);
+        mxm = std::max(mxm, (long long)n->Mp[l]);
+    }
+    p.part = off;
+    off += rup((long long)p.n_chunks * mxo * 4, 256);
+    p.bpart = off;
+    off += rup((long long)p.n_chunks * mxm * 4, 256);
+    p.total = off;
+}
+
+size_t marf_step_saved_bytes(const marf_net* net, const marf_geometry* geo) {
+    GeoDev g;
+    if (!net || !geo || geo->mode != MARF_GEO_GRID || make_geo(geo, g, MARF_TILE_PAD) != MARF_OK) return 0;
+    StepPlan p;
+    plan_step(net, (long long)g.B * g.Np_pad, p);
+    return p.total;
+}
+
+int marf_step_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
+                      const float* d_gt, const float* d_mask, const float* d_denom_override, float* d_rgb,
+                      float* d_loss_out, void* d_saved, void* stream) {
+    if (!net || !d_packed || !d_gt || !d_loss_out || !d_saved) return fail(MARF_ERR_INVALID, "step_forward: NULL argument");
+    if (!geo || geo->mode != MARF_GEO_GRID) return fail(MARF_ERR_INVALID, "step_forward: needs the grid geometry");
+    hipStream_t s = (hipStream_t)stream;
+    StepArgs a;
+    memset(&a, 0, sizeof(a));
+    int rc = make_geo(geo, a.geo, MARF_TILE_PAD);
+    if (rc) return rc;
+    fill_netdev(net, d_packed, a.net);
+    a.c2f = make_c2f(c2f);
+    a.rgb = d_rgb;
+    a.gt = d_gt;
+    a.mask = d_mask;
+    a.S = (long long)a.geo.B * a.geo.Np_pad;
+    a.lda = net->lda;
+    StepPlan p;
+    plan_step(net, a.S, p);
+    char* sv = (char*)d_saved;
+    const int nl = net->n_layers;
+    for (int l = 0; l < nl - 1; ++l) a.feat[l] = sv + p.feat[l];
+    for (int l = 1; l < nl; ++l) {
+        a.dz[l] = sv + p.dz[l];
+        a.mask_bits[l] = (uint64_t*)(sv + p.mask[l]);
+    }
+    a.wlast_partial = (float*)(sv + p.wlast);
+    a.blast_partial = (float*)(sv + p.blast);
+    a.dH_partial = (float*)(sv + p.dH);
+    a.loss_partial = (double*)(sv + p.loss);
+    {
+        MarfProfScope ps("mlp_step", s);
+        HIPCHK(marf_launch_mlp_step(a, net->dtype, net->TP, net->lds_step, p.n_tiles, s), "step_forward");
+    }
+    {
+        MarfProfScope ps("loss_final", s);
+        HIPCHK(marf_launch_loss_final(a.loss_partial, p.n_tiles, d_loss_out, d_denom_override, s), "step_forward loss");
+    }
+    return MARF_OK;
+}
+
+int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void* d_saved, const float* d_h_params,
+                       int lie_batch, const float* d_gout, const float* d_loss_out, float* d_dparams, float* d_dh,
+                       void* stream) {
+    if (!net || !d_saved || !d_gout || !d_loss_out) return fail(MARF_ERR_INVALID, "step_backward: NULL argument");
+    if (!geo || geo->mode != MARF_GEO_GRID) return fail(MARF_ERR_INVALID, "step_backward: needs the grid geometry");
+    if (d_dh && !d_h_params) return fail(MARF_ERR_INVALID, "step_backward: d_dh requested without the warp parameters");
+    hipStream_t s = (hipStream_t)stream;
+    GeoDev g;
+    int rc = make_geo(geo, g, MARF_TILE_PAD);
+    if (rc) return rc;
+    const long long S = (long long)g.B * g.Np_pad;
+    StepPlan p;
+    plan_step(net, S, p);
+    const char* sv = (const char*)d_saved;
+    float* part = (float*)(sv + p.part);
+    float* bpart = (float*)(sv + p.bpart);
+    const float* denom = d_loss_out + 1;
+    const int nl = net->n_layers;
+    if (d_dparams) {
+        for (int l = 0; l < nl - 1; ++l) {
+            {
+                MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
+                HIPCHK(marf_launch_wgrad(net->dtype, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], net->Kp[l], S,
+                                         net->Mp[l], net->Kp[l], p.chunk, p.n_chunks, part, bpart, s),
+                       "step_backward wgrad");
+            }
+            {
+                MarfProfScope ps("wgrad_reduce", s);
+                HIPCHK(marf_launch_wgrad_reduce(part, bpart, p.n_chunks, net->Mp[l], net->Kp[l], net->dims[l + 1],
+                                                net->dims[l], d_dparams + net->w_off[l], d_dparams + net->b_off[l], s,
+                                                d_gout, denom),
+                       "step_backward wgrad reduce");
+            }
+        }
+        const int l = nl - 1;
+        MarfProfScope ps("wgrad_last_reduce", s);
+        HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.wlast), (const float*)(sv + p.blast), p.n_tiles, 3,
+                                        net->Kp[l], 3, net->dims[l], d_dparams + net->w_off[l],
+                                        d_dparams + net->b_off[l], s, d_gout, denom),
+               "step_backward last reduce");
+    }
+    if (d_dh) {
+        MarfProfScope ps("warp_bwd", s);
+        HIPCHK(marf_launch_reduce_dH((const float*)(sv + p.dH), g.Np_pad / net->TP, g.B, d_h_params, nullptr, d_dh,
+                                     lie_batch > 0 ? lie_batch : g.B, s, d_gout, denom),
+               "step_backward warp");
     }
     return MARF_OK;
 }

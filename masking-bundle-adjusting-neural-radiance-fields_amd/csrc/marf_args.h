@@ -36,6 +36,26 @@ struct BwdArgs {
     int lda;
 };
 
+// Fused training step of the grid geometry (marf_step.hip): forward, masked MSE with unit upstream
+// gradient, dgrad chain and warp adjoint in one pass over each tile.
+struct StepArgs {
+    NetDev net;
+    GeoDev geo;
+    C2fDev c2f;
+    float* rgb;                             // [B][Np][3] forward output (may be null)
+    const float* gt;                        // [B][3][Np] target
+    const float* mask;                      // [B][1][Np] or null (plain mean)
+    void* feat[MARF_MAX_LAYERS];            // out: inputs of layers 0 .. n-2 [S][Kp_l]
+    uint64_t* mask_bits[MARF_MAX_LAYERS];   // scratch: ReLU masks of feat_l, l = 1 .. n-1
+    void* dz[MARF_MAX_LAYERS];              // out: dz_l, l = 1 .. n-1 [S][Kp_l]
+    float* wlast_partial;                   // out: [n_tiles][3][Kp_{n-1}] last-layer weight gradient
+    float* blast_partial;                   // out: [n_tiles][3]
+    float* dH_partial;                      // out: [n_tiles][9]
+    double* loss_partial;                   // out: [n_tiles][2] = sum ((p - g) m)^2, sum m
+    long long S;
+    int lda;
+};
+
 struct PackLayer {
     int M, K;                            // true dims (nn.Linear weight [M][K])
     int Mp, Kp, Mt;                      // padded: Wf [Mp][Kp], Wt [Kp][Mt], bias [Mp]
@@ -53,7 +73,8 @@ struct PackArgs {
 hipError_t marf_launch_sl3(const float* h, float* H, int B, int batch_hint, hipStream_t s);
 hipError_t marf_launch_sl3_bwd(const float* h, const float* dH, float* dh, int B, int batch_hint, hipStream_t s);
 hipError_t marf_launch_reduce_dH(const float* partial, int tiles_per_patch, int B, const float* h, float* dH_out,
-                                 float* dh, int batch_hint, hipStream_t s);
+                                 float* dh, int batch_hint, hipStream_t s, const float* gscale = nullptr,
+                                 const float* denom = nullptr);
 hipError_t marf_launch_mlp_fwd(const marf::FwdArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
 hipError_t marf_launch_mlp_bwd(const marf::BwdArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
 hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
@@ -61,7 +82,10 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
 hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* feat, long long S, int ldf, int K,
                                   int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s);
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
-                                    int Ko, float* dW, float* db, hipStream_t s);
+                                    int Ko, float* dW, float* db, hipStream_t s, const float* gscale = nullptr,
+                                    const float* denom = nullptr);
+hipError_t marf_launch_mlp_step(const marf::StepArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
+hipError_t marf_launch_loss_final(const double* part, int n, float* out, const float* denom_override, hipStream_t s);
 hipError_t marf_launch_mse(const float* pred, const float* gt, const float* mask, int B, int Np, double* part,
                            float* out, const float* denom_override, hipStream_t s);
 hipError_t marf_launch_mse_bwd(const float* pred, const float* gt, const float* mask, int B, int Np,

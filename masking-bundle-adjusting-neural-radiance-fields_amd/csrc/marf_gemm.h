@@ -1,0 +1,426 @@
+// marf_gemm.h -- device building blocks shared by the per-tile MLP kernels (marf_mlp.hip,
+// marf_step.hip): the LDS-resident activation tile GEMM (weights = MFMA A operand streamed from
+// L2, activations = B operand read from LDS), its epilogue store and tile addressing.
+//
+// Orientation: Z^T[out x px] = W[out x in] . A^T[in x px]: lane = output row / 8 contiguous k for
+// the weights, lane = pixel / 8 contiguous features for the activations; the accumulator holds a
+// pixel per lane and features in registers.  256 threads = 4 waves; output row tiles (32) of a
+// layer are dealt round-robin to the 4 waves, each wave covers all PT = TP/32 pixel tiles.
+#pragma once
+#include "marf_args.h"
+
+namespace marf {
+
+template <class P>
+MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int cols, typename P::T* dst, int ldd) {
+    // LDS [rows][lda] -> global [rows][ldd], first `cols` columns. bf16: 16-byte chunks.
+    // The (row, chunk) walk is incremental: one division per call, none per element.
+    typedef typename P::T T;
+    if (sizeof(T) == 2) {
+        const int nch = cols / 8;
+        const int step = blockDim.x, dr = step / nch, dc = step - dr * nch;
+        int r = threadIdx.x / nch, c = threadIdx.x - r * nch;
+        for (; r < rows;) {
+            uint4 v = *reinterpret_cast<const uint4*>(act + (size_t)r * lda + 8 * c);
+            *reinterpret_cast<uint4*>(dst + (size_t)r * ldd + 8 * c) = v;
+            r += dr;
+            c += dc;
+            if (c >= nch) {
+                c -= nch;
+                ++r;
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
+            int r = e / cols, c = e - r * cols;
+            dst[(size_t)r * ldd + c] = act[(size_t)r * lda + c];
+        }
+    }
+}
+
+// acc[i][PT] += W[rows (wave + 4 i)*32 .., k] . act[px, k]^T over k < K for the NA row tiles this
+// wave owns (i < NA).  NA is dispatched once per layer (wave-uniform), so the body is branch-free.
+//
+// Schedule: the weight fragments stream from L2 through a static 4-deep register ring (slot u is
+// reloaded for k-step k+4 right after its MFMAs issue: three k-steps of latency cover, no register
+// moves), the activation fragments of step k+1 are read from LDS while step k's MFMAs run (two
+// statically named buffers).  Loads past the last k-step are clamped to it (harmless L2 hits).
+template <class P, int NA, int RT, int PT>
+MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__ W, int K,
+                        const typename P::T* act, int lda, int wave, int lane) {
+    typedef typename P::frag F;
+    const int ko = P::kofs(lane);
+    const int rl = lane & 31;
+    const int nk = K / P::KS;
+    const typename P::T* wrow[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) wrow[i] = W + (size_t)((wave + 4 * i) * 32 + rl) * K + ko;
+    const typename P::T* brow = act + (size_t)rl * lda + ko;
+    auto ldA = [&](F (&dst)[NA], int k) {
+        const int kc = (k < nk ? k : nk - 1) * P::KS;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) dst[i] = P::load_frag(wrow[i] + kc);
+    };
+    auto ldB = [&](F (&dst)[PT], int k) {
+        const int kc = (k < nk ? k : nk - 1) * P::KS;
+#pragma unroll
+        for (int j = 0; j < PT; ++j) dst[j] = P::load_frag(brow + (size_t)j * 32 * lda + kc);
+    };
+    auto mma = [&](const F (&a)[NA], const F (&b)[PT]) {
+#pragma unroll
+        for (int j = 0; j < PT; ++j)
+#pragma unroll
+            for (int i = 0; i < NA; ++i) acc[i][j] = P::mma32(a[i], b[j], acc[i][j]);
+    };
+    F A0[NA], A1[NA], A2[NA], A3[NA], B0[PT], B1[PT];
+    if constexpr (sizeof(F) * NA > 32) {
+        // wide row blocks (bf16, NA > 2): a 2-deep ring keeps the kernel inside 256 VGPRs
+        ldA(A0, 0);
+        ldA(A1, 1);
+        ldB(B0, 0);
+        int k = 0;
+        for (; k + 2 <= nk; k += 2) {
+            ldB(B1, k + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(A0, B0);
+            __builtin_amdgcn_sched_barrier(0);
+            ldA(A0, k + 2);
+            ldB(B0, k + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(A1, B1);
+            __builtin_amdgcn_sched_barrier(0);
+            ldA(A1, k + 3);
+        }
+        if (k < nk) mma(A0, B0);
+        return;
+    }
+    ldA(A0, 0);
+    ldA(A1, 1);
+    ldA(A2, 2);
+    ldA(A3, 3);
+    ldB(B0, 0);
+    int k = 0;
+    // sched_barrier pins the issue order: left alone, the scheduler sinks every weight load to
+    // the loop end (one MFMA of latency cover) and folds the two B buffers into one.
+    for (; k + 4 <= nk; k += 4) {
+        ldB(B1, k + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A0, B0);
+        __builtin_amdgcn_sched_barrier(0);
+        ldA(A0, k + 4);
+        ldB(B0, k + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A1, B1);
+        __builtin_amdgcn_sched_barrier(0);
+        ldA(A1, k + 5);
+        ldB(B1, k + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A2, B0);
+        __builtin_amdgcn_sched_barrier(0);
+        ldA(A2, k + 6);
+        ldB(B0, k + 4);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A3, B1);
+        __builtin_amdgcn_sched_barrier(0);
+        ldA(A3, k + 7);
+    }
+    // remainder (nk % 4 steps): A0..A2 hold steps k..k+2, B0 holds step k
+    if (k < nk) {
+        ldB(B1, k + 1);
+        mma(A0, B0);
+        if (k + 1 < nk) {
+            ldB(B0, k + 2);
+            mma(A1, B1);
+            if (k + 2 < nk) mma(A2, B0);
+        }
+    }
+}
+
+// Accumulators start at the bias of their output row when `bias` is given (so the epilogue does
+// not add it), else at zero.
+template <class P, int RT, int PT>
+MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__ W, int K, int n_rt,
+                        const typename P::T* act, int lda, int wave, int lane, const float* bias = nullptr) {
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+        f32x16 init = (f32x16){};
+        const int rt = wave + 4 * i;
+        if (bias && rt < n_rt) {
+            const float* bb = bias + rt * 32 + 4 * (lane >> 5);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 bv = *reinterpret_cast<const float4*>(bb + 8 * q);
+                init[4 * q] = bv.x;
+                init[4 * q + 1] = bv.y;
+                init[4 * q + 2] = bv.z;
+                init[4 * q + 3] = bv.w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PT; ++j) acc[i][j] = init;
+    }
+    int na = (n_rt - wave + 3) / 4;
+    na = na < 0 ? 0 : (na > RT ? RT : na);
+    switch (na) {
+        case 1: gemm_rows<P, 1, RT, PT>(acc, W, K, act, lda, wave, lane); break;
+        case 2: gemm_rows<P, 2, RT, PT>(acc, W, K, act, lda, wave, lane); break;
+        case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT>(acc, W, K, act, lda, wave, lane); break;
+        case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT>(acc, W, K, act, lda, wave, lane); break;
+        default: break;
+    }
+}
+
+// Store 4 consecutive rows (features) of one accumulator group for this lane's pixel.
+template <class P>
+MARF_DEV void store4(typename P::T* dst, float x0, float x1, float x2, float x3) {
+    if (sizeof(typename P::T) == 2) {
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        uint2 v;  // one v_cvt_pk_bf16_f32 per pair (RNE)
+        v.x = __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){x0, x1}), bf16x2));
+        v.y = __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){x2, x3}), bf16x2));
+        *reinterpret_cast<uint2*>(dst) = v;
+    } else {
+        float* d = reinterpret_cast<float*>(dst);
+        d[0] = x0;
+        d[1] = x1;
+        d[2] = x2;
+        d[3] = x3;
+    }
+}
+
+MARF_DEV void tile_origin(const GeoDev& g, int tile, int TP, int& b, int& p0, long long& slot0) {
+    int tpp = g.Np_pad / TP;
+    b = tile / tpp;
+    p0 = (tile - b * tpp) * TP;
+    slot0 = (long long)b * g.Np_pad + p0;
+}
+
+
+// ======================================================================== per-tile phases
+
+// BARF coarse-to-fine weight of every band into LDS (model/planar.py:462-470); 1 without c2f.
+MARF_DEV void c2f_weights_lds(const C2fDev& c2f, int L, float* wsh) {
+    if ((int)threadIdx.x < L)
+        wsh[threadIdx.x] = c2f.on ? c2f_weight(*c2f.progress, c2f.start, c2f.span, L, threadIdx.x) : 1.0f;
+}
+
+// Prologue: pixel grid -> sl(3) warp -> posenc (+c2f) of the tile's TP slots -> act [TP][Kp0]
+// (warp.py:33-81, model/planar.py:451-471; feature layout [u, v, sin_k(u), cos_k(u), sin_k(v),
+// cos_k(v)], zero padded to Kp0).  256 / TP threads share a pixel, bands dealt round-robin.
+template <class P, int TP>
+MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh,
+                            typename P::T* act, int lda, int b, int p0) {
+    constexpr int NPART = 256 / TP;
+    const int L = net.L;
+    const int i = threadIdx.x % TP, part = threadIdx.x / TP;
+    float x, y, u = 0.f, v = 0.f, X[3];
+    slot_point(geo, b, p0 + i, x, y, u, v, X);
+    typename P::T* row = act + (size_t)i * lda;
+    if (part == NPART - 1) {
+        row[0] = P::cvt(u);
+        row[1] = P::cvt(v);
+    }
+    // band q = c*L + k of coordinate c: sin at 2 + 2cL + k, cos at 2 + 2cL + L + k
+    for (int q = part; q < 2 * L; q += NPART) {
+        const int c = q >= L, k = q - c * L;
+        float s, co;
+        band_sincos<sizeof(typename P::T) == 2>(c ? v : u, k, s, co);
+        if (c2f_on) {
+            const float w = wsh[k];
+            s = s * w;
+            co = co * w;
+        }
+        row[2 + q + c * L] = P::cvt(s);
+        row[2 + q + c * L + L] = P::cvt(co);
+    }
+    for (int f = net.D + part; f < net.Kp[0]; f += NPART) row[f] = P::cvt(0.f);
+}
+
+// Hidden-layer epilogue: ReLU of the accumulators (bias already in them) written back to act in
+// place, and (mk != null) the ReLU masks: per (pixel tile, row tile) 128 contiguous bytes = the 16
+// wave ballots (one per accumulator register), gathered into lanes 0..31 of one VGPR by
+// v_writelane and written with one vector store.
+template <class P, int RT, int PT>
+MARF_DEV void relu_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, int n_rt, int wave, int lane,
+                            uint64_t* mk, long long slot0) {
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+        const int rt = wave + 4 * i;
+        if (rt >= n_rt) continue;
+        const int rbase = rt * 32 + 4 * (lane >> 5);
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const int px = j * 32 + (lane & 31);
+            float o[16];
+            uint64_t bal[16];  // the v_cmp results themselves (SGPR pairs)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float z = acc[i][j][r];
+                const bool pos = z > 0.f;
+                o[r] = pos ? z : 0.f;
+                bal[r] = __ballot(pos);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                store4<P>(act + (size_t)px * lda + rbase + 8 * q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+            if (mk) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"((uint32_t)bal[r]), "n"(2 * r));
+                    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"((uint32_t)(bal[r] >> 32)), "n"(2 * r + 1));
+                }
+                uint32_t* mrow = reinterpret_cast<uint32_t*>(mk + (((slot0 >> 5) + j) * n_rt + rt) * 16);
+                if (lane < 32) mrow[lane] = w;
+            }
+        }
+    }
+}
+
+// Dgrad epilogue: dz = acc * relu'(feat) with the masks saved by relu_epilogue, written to act.
+// The 16 wave-uniform lane masks of a tile come in with two scalar loads; each element is one
+// v_cndmask.
+template <class P, int RT, int PT>
+MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, int n_rt, int wave, int lane,
+                            const uint64_t* mk, long long slot0) {
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+        const int rt = wave + 4 * i;
+        if (rt >= n_rt) continue;
+        const int rbase = rt * 32 + 4 * (lane >> 5);
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const int px = j * 32 + (lane & 31);
+            const uint64_t* mrow = mk + (((slot0 >> 5) + j) * n_rt + rt) * 16;
+            u32x16 m0, m1;
+            asm volatile(
+                "s_load_dwordx16 %0, %2, 0x0\n\t"
+                "s_load_dwordx16 %1, %2, 0x40\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&s"(m0), "=&s"(m1)
+                : "s"(mrow)
+                : "memory");
+            float o[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const uint32_t lo = r < 8 ? m0[2 * r] : m1[2 * r - 16];
+                const uint32_t hi = r < 8 ? m0[2 * r + 1] : m1[2 * r - 15];
+                const uint64_t ms = ((uint64_t)hi << 32) | lo;
+                float v;
+                asm volatile("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(v) : "v"(acc[i][j][r]), "s"(ms));
+                o[r] = v;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                store4<P>(act + (size_t)px * lda + rbase + 8 * q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+        }
+    }
+}
+
+// Layer-0 dgrad (d feat_0 = W_0^T dz_1, act holds dz_1) and the posenc / projective-warp adjoint
+// (model/planar.py:451-471, warp.py:74-78 backward): per slot d(u, v), then for the grid geometry
+// d(Hx) and one dH[3x3] partial per tile (fixed-order wave + block sums); for explicit coordinates
+// d coords.  `red` needs 4 * TP * 2 floats, `red9` 4 * 9.  smem = the act tile (reused as fp32).
+template <class P, int TP>
+MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh, char* smem, int lda,
+                           int wave, int lane, int b, int p0, float* red, float* red9, float* dH_partial,
+                           float* d_coords) {
+    typedef typename P::T T;
+    constexpr int PT = TP / 32;
+    constexpr int RT = 8 / PT;
+    const int L = net.L;
+    const T* act = reinterpret_cast<const T*>(smem);
+    const int R = net.Kp[0], Kk = net.Mt[0], n_rt = R / 32;
+    f32x16 acc[RT][PT];
+    gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[0]), Kk, n_rt, act, lda, wave, lane);
+    __syncthreads();
+    float* df = reinterpret_cast<float*>(smem);
+    const int ldf = R + 1;
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+        const int rt = wave + 4 * i;
+        if (rt >= n_rt) continue;
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const int px = j * 32 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) df[(size_t)px * ldf + rt * 32 + acc_row(lane, r)] = acc[i][j][r];
+        }
+    }
+    __syncthreads();
+
+    // posenc adjoint: d coord_c = df[c] + sum_k w_k f_k (cos(x_k) df_sin - sin(x_k) df_cos)
+    constexpr int NPART = 256 / TP;
+    const int i = threadIdx.x % TP, part = threadIdx.x / TP;
+    float x, y, u = 0.f, v = 0.f, X[3] = {0.f, 0.f, 1.f};
+    const bool valid = slot_point(geo, b, p0 + i, x, y, u, v, X);
+    const float* row = df + (size_t)i * ldf;
+    float du = 0.f, dv = 0.f;
+    if (part == 0) {
+        du += row[0];
+        dv += row[1];
+    }
+    for (int q = part; q < 2 * L; q += NPART) {
+        const int c = q >= L, k = q - c * L;
+        float s, co;
+        band_sincos<sizeof(T) == 2>(c ? v : u, k, s, co);
+        float gs = row[2 + q + c * L], gc = row[2 + q + c * L + L];
+        if (c2f_on) {
+            const float w = wsh[k];
+            gs = gs * w;
+            gc = gc * w;
+        }
+        float dspec = gs * co - gc * s;
+        float d = dspec * ldexpf(3.14159265358979323846f, k);
+        if (c == 0) du += d; else dv += d;
+    }
+    red[(part * TP + i) * 2] = du;
+    red[(part * TP + i) * 2 + 1] = dv;
+    __syncthreads();
+    float h9[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) h9[e] = 0.f;
+    if ((int)threadIdx.x < TP) {
+        du = red[i * 2];
+        dv = red[i * 2 + 1];
+        for (int q = 1; q < NPART; ++q) {
+            du += red[(q * TP + i) * 2];
+            dv += red[(q * TP + i) * 2 + 1];
+        }
+        if (geo.mode == 1) {
+            if (valid && d_coords) {
+                d_coords[2 * (size_t)(p0 + i)] = du;
+                d_coords[2 * (size_t)(p0 + i) + 1] = dv;
+            }
+        } else if (valid) {
+            // (u, v) = X[:2] / (X[2] + 1e-8): torch div backward, then bmm backward
+            float dd = X[2] + 1e-8f;
+            float dX0 = du / dd, dX1 = dv / dd;
+            float dd2 = dd * dd;
+            float dX2 = (-du * X[0]) / dd2 + (-dv * X[1]) / dd2;
+            const float hom[3] = {x, y, 1.f};
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                h9[0 + c] = dX0 * hom[c];
+                h9[3 + c] = dX1 * hom[c];
+                h9[6 + c] = dX2 * hom[c];
+            }
+        }
+    }
+    if (geo.mode == 0) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) {
+            float s = wave_sum(h9[e]);
+            if (lane == 0) red9[wave * 9 + e] = s;
+        }
+        __syncthreads();
+        if (threadIdx.x < 9) {
+            float s = red9[threadIdx.x];
+            for (int w = 1; w < 4; ++w) s += red9[w * 9 + threadIdx.x];
+            dH_partial[(size_t)blockIdx.x * 9 + threadIdx.x] = s;
+        }
+    }
+}
+
+}  // namespace marf

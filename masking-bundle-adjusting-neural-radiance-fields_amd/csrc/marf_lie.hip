@@ -270,7 +270,8 @@ __global__ void k_sl3_backward(const float* __restrict__ h, const float* __restr
 // overwrite).
 __global__ void k_reduce_dH_lie_bwd(const float* __restrict__ partial, int tiles_per_patch,
                                     const float* __restrict__ h, float* __restrict__ dH_out,
-                                    float* __restrict__ dh, int batch_hint) {
+                                    float* __restrict__ dh, int batch_hint, const float* __restrict__ gscale,
+                                    const float* __restrict__ denom) {
     __shared__ double red[64][9];
     int b = blockIdx.x;
     int t = threadIdx.x;
@@ -288,6 +289,9 @@ __global__ void k_reduce_dH_lie_bwd(const float* __restrict__ partial, int tiles
             for (int i = 0; i < 64; ++i) s += red[i][e];
             dHf[e] = (float)s;
         }
+        // fused step: partials carry the unit-upstream gradient without 1/denominator
+        if (gscale)
+            for (int e = 0; e < 9; ++e) dHf[e] = dHf[e] * (gscale[0] / denom[0]);
         if (dH_out)
             for (int e = 0; e < 9; ++e) dH_out[9 * b + e] = dHf[e];
         if (dh) {
@@ -315,9 +319,10 @@ hipError_t marf_launch_sl3_bwd(const float* h, const float* dH, float* dh, int B
 }
 
 hipError_t marf_launch_reduce_dH(const float* partial, int tiles_per_patch, int B, const float* h,
-                                 float* dH_out, float* dh, int batch_hint, hipStream_t s) {
+                                 float* dH_out, float* dh, int batch_hint, hipStream_t s, const float* gscale,
+                                 const float* denom) {
     if (B <= 0) return hipSuccess;
     hipLaunchKernelGGL(marf::k_reduce_dH_lie_bwd, dim3(B), dim3(64), 0, s, partial, tiles_per_patch, h, dH_out, dh,
-                       batch_hint);
+                       batch_hint, gscale, denom);
     return hipGetLastError();
 }

@@ -1,0 +1,273 @@
+// marf_step.hip -- the fused training step of the planar render loop on gfx950.
+//
+// One block = one tile of TP pixel slots of the crop grid.  Because the target and the mask are
+// known when Graph.forward runs (model/planar.py:329-336 -> compute_loss :355-391), the tile's whole
+// forward AND backward run in one pass, activations resident in one LDS tile:
+//
+//   grid -> sl(3) warp -> posenc + c2f                 (warp.py:33-81, model/planar.py:451-471)
+//   (Linear + ReLU) x (n-1) -> Linear -> sigmoid       (model/planar.py:429-449)      -> rgb
+//   masked MSE: loss partial, d rgb = 2 (p - g) m m    (model/planar.py:382-391), unit upstream
+//                                                       gradient and no 1/denominator: both
+//                                                       multiply every gradient and are applied
+//                                                       in the reduction kernels (gout / denom)
+//   sigmoid' -> last-layer weight gradient (16x16 MFMA over the tile's pixels, feat_{n-1} is
+//   still in LDS) -> dgrad chain W_l^T with the ReLU masks -> dz_l saved for the hidden-layer
+//   weight gradients -> layer-0 dgrad -> posenc / warp adjoint -> dH[3x3] partial per tile.
+//
+// HBM traffic per pixel (bf16, C3: L=16, 4 x 256 hidden): writes feat_0..feat_{n-2} and
+// dz_1..dz_{n-1} (192 + 3*512 + 4*512 B), the ReLU masks (4 * 32 B, read back by the same wave)
+// and rgb (12 B); reads target + mask (16 B).  Against the separate forward / loss / backward
+// kernels this drops the last layer's input (written and read back, 1 KB), rgb / d rgb round
+// trips and a second prologue.
+#include "marf_gemm.h"
+
+namespace marf {
+
+// Transposed LDS read (gfx950 ds_read_b64_tr_b16): per 16-lane group, a 4 x 16 block of bf16 is
+// read row-major (lane gi addresses row gi >> 2, columns 4 (gi & 3) ..) and delivered
+// column-major: lane gi receives column gi of the 4 rows.
+MARF_DEV i16x4 tr_read16(const u16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
+}
+
+template <class P, int TP>
+__global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
+    typedef typename P::T T;
+    constexpr int PT = TP / 32;
+    constexpr int RT = 8 / PT;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* act = reinterpret_cast<T*>(smem);
+    __shared__ float wsh[32];
+    __shared__ float red[4 * TP * 2];
+    __shared__ float red9[4 * 9];
+    __shared__ __attribute__((aligned(16))) float gl[TP][4];  // sigmoid' gradient per slot (fp32)
+    __shared__ __attribute__((aligned(16))) T gT[4][TP];      // the same, channel-major, MFMA operand
+    __shared__ float lsum[2][TP];                              // per-slot ((p-g) m)^2 and m
+
+    const NetDev& net = a.net;
+    const int lda = a.lda;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int b, p0;
+    long long slot0;
+    tile_origin(a.geo, blockIdx.x, TP, b, p0, slot0);
+    const int nl = net.n_layers;
+    const int Np = a.geo.Np;
+
+    c2f_weights_lds(a.c2f, net.L, wsh);
+    __syncthreads();
+    tile_prologue<P, TP>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0);
+    __syncthreads();
+    copy_tile_out<P>(act, lda, TP, net.Kp[0], reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0]);
+
+    // ---- hidden layers (forward)
+    for (int l = 0; l < nl - 1; ++l) {
+        const int K = net.Kp[l], M = net.Mp[l], n_rt = M / 32;
+        f32x16 acc[RT][PT];
+        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l]);
+        __syncthreads();  // every wave has consumed the layer input
+        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], slot0);
+        __syncthreads();
+        if (l + 1 < nl - 1)  // the last layer's input never leaves LDS
+            copy_tile_out<P>(act, lda, TP, M, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M);
+    }
+
+    // ---- last layer (3 outputs, rows padded to 16): 16x16 MFMA, TP/4 pixels per wave, sigmoid,
+    //      rgb, masked-MSE partial and d rgb, sigmoid backward -> gl
+    const int Kl = net.Kp[nl - 1];
+    {
+        const T* W = reinterpret_cast<const T*>(net.Wf[nl - 1]);
+        constexpr int NJ = TP / 64;
+        f32x4 acc[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] = (f32x4){};
+        const int ko = P::kofs16(lane);
+        for (int k0 = 0; k0 < Kl; k0 += P::KS16) {
+            typename P::frag wa = P::load_frag(W + (size_t)(lane & 15) * Kl + k0 + ko);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int px = wave * (TP / 4) + j * 16 + (lane & 15);
+                typename P::frag bb = P::load_frag(act + (size_t)px * lda + k0 + ko);
+                acc[j] = P::mma16(wa, bb, acc[j]);
+            }
+        }
+        if (lane < 16) {
+            const float* bl = net.bias[nl - 1];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int px = wave * (TP / 4) + j * 16 + lane;
+                const int p = p0 + px;
+                float g[3] = {0.f, 0.f, 0.f};
+                float sq = 0.f, mv = 0.f;
+                if (p < Np) {
+                    const float m = a.mask ? a.mask[(size_t)b * Np + p] : 1.0f;
+                    float* o = a.rgb ? a.rgb + ((size_t)b * Np + p) * 3 : nullptr;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const float z = acc[j][c] + bl[c];
+                        const float y = 1.0f / (1.0f + expf(-z));
+                        if (o) o[c] = y;
+                        // model/planar.py:388-390 and its autograd: x = (p - g) m, d = 2 x m
+                        const float x = (y - a.gt[((size_t)b * 3 + c) * Np + p]) * m;
+                        sq += x * x;
+                        const float d = (2.0f * x) * m;
+                        g[c] = (d * (1.0f - y)) * y;  // torch sigmoid_backward
+                    }
+                    mv = m;
+                }
+                *reinterpret_cast<float4*>(&gl[px][0]) = make_float4(g[0], g[1], g[2], 0.f);
+                gT[0][px] = P::cvt(g[0]);
+                gT[1][px] = P::cvt(g[1]);
+                gT[2][px] = P::cvt(g[2]);
+                gT[3][px] = P::cvt(0.f);
+                lsum[0][px] = sq;
+                lsum[1][px] = mv;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- masked-MSE partial of the tile (fp64, fixed order) and the last bias gradient
+    if (wave == 0) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int px = lane; px < TP; px += 64) {
+            s0 += (double)lsum[0][px];
+            s1 += (double)lsum[1][px];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            s0 += __shfl_xor(s0, o, 64);
+            s1 += __shfl_xor(s1, o, 64);
+        }
+        if (lane == 0) {
+            a.loss_partial[2 * (size_t)blockIdx.x] = s0;
+            a.loss_partial[2 * (size_t)blockIdx.x + 1] = s1;
+        }
+    } else if (wave == 1) {
+        float s[3] = {0.f, 0.f, 0.f};
+        for (int px = lane; px < TP; px += 64)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) s[c] += gl[px][c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float t = wave_sum(s[c]);
+            if (lane == c) a.blast_partial[(size_t)blockIdx.x * 3 + c] = t;
+        }
+    }
+
+    // ---- last-layer weight gradient of the tile: dW[c][k] = sum_px g[px][c] feat[px][k]
+    //      16x16 MFMA, A = g^T (channels x pixels), B = feat (pixels x features, transposed LDS
+    //      read for bf16); column tiles of 16 features dealt round-robin to the waves.
+    {
+        float* wout = a.wlast_partial + (size_t)blockIdx.x * 3 * Kl;
+        for (int ct = wave; ct < Kl / 16; ct += 4) {
+            f32x4 acc = (f32x4){};
+            if constexpr (sizeof(T) == 2) {
+                const int g = lane >> 4, gi = lane & 15;
+#pragma unroll
+                for (int k0 = 0; k0 < TP; k0 += 32) {
+                    bf16x8 fa;
+                    if (gi < 4) fa = *reinterpret_cast<const bf16x8*>(&gT[gi][k0 + 8 * g]);
+                    else fa = (bf16x8){};
+                    const int r0 = k0 + 8 * g + (gi >> 2);
+                    const u16* base = reinterpret_cast<const u16*>(act) + (size_t)r0 * lda + ct * 16 + 4 * (gi & 3);
+                    i16x4 v[2] = {tr_read16(base), tr_read16(base + 4 * lda)};
+                    acc = P::mma16(fa, *reinterpret_cast<bf16x8*>(v), acc);
+                }
+            } else {
+                const int kk = lane >> 4, n = lane & 15;
+                for (int k0 = 0; k0 < TP; k0 += 4) {
+                    const float fa = n < 4 ? P::tof(gT[n][k0 + kk]) : 0.f;
+                    const float fb = P::tof(act[(size_t)(k0 + kk) * lda + ct * 16 + n]);
+                    acc = P::mma16(fa, fb, acc);
+                }
+            }
+            // accumulator: lane l, reg r -> row (channel) 4 (l >> 4) + r, column l & 15
+            if (lane < 16) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) wout[(size_t)c * Kl + ct * 16 + lane] = acc[c];
+            }
+        }
+    }
+    __syncthreads();  // feat_{n-1} consumed
+
+    // ---- d (last-layer input) operand: act[px][0 .. Mt) = g
+    if ((int)threadIdx.x < TP) {
+        const int i = threadIdx.x;
+        T* row = act + (size_t)i * lda;
+        const int Kt = net.Mt[nl - 1];
+        for (int c = 0; c < Kt; ++c) row[c] = P::cvt(c < 3 ? gl[i][c] : 0.f);
+    }
+    // the ReLU mask records were written by this same wave with vector stores: drain them to L2
+    // before the scalar loads of the dgrad epilogues read them back
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // ---- dgrad chain, l = n-1 .. 1 : dfeat_l = W_l^T dz_{l+1}; dz_l = dfeat_l * relu'(feat_l)
+    for (int l = nl - 1; l >= 1; --l) {
+        const int R = net.Kp[l], Kk = net.Mt[l], n_rt = R / 32;
+        f32x16 acc[RT][PT];
+        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane);
+        __syncthreads();
+        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l], slot0);
+        __syncthreads();
+        copy_tile_out<P>(act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, R);
+    }
+
+    // ---- layer-0 dgrad + posenc / warp adjoint -> dH partial
+    warp_adjoint<P, TP>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr);
+}
+
+// Loss of the fused step from the per-tile partials (fp64, fixed-order tree):
+// out[0] = f32(sum x^2) / denom, out[1] = denom (= denom_override or 3 * f32(sum m)),
+// out[2] = local 3 * f32(sum m)  (model/planar.py:390, as k_mse_final).
+__global__ __launch_bounds__(256) void k_loss_final(const double* __restrict__ part, int n, float* __restrict__ out,
+                                                    const float* __restrict__ denom_override) {
+    __shared__ double rn[256], rm[256];
+    double num = 0.0, ms = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        num += part[2 * (size_t)i];
+        ms += part[2 * (size_t)i + 1];
+    }
+    rn[threadIdx.x] = num;
+    rm[threadIdx.x] = ms;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            rn[threadIdx.x] += rn[threadIdx.x + o];
+            rm[threadIdx.x] += rm[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float denom = denom_override ? denom_override[0] : (float)rm[0] * 3.0f;
+        out[0] = (float)rn[0] / denom;
+        out[1] = denom;
+        out[2] = (float)rm[0] * 3.0f;
+    }
+}
+
+}  // namespace marf
+
+using namespace marf;
+
+template <class P, int TP>
+static hipError_t launch_step_t(const StepArgs& a, size_t lds, int n_tiles, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_mlp_step<P, TP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_mlp_step<P, TP>), dim3(n_tiles), dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_mlp_step(const StepArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s) {
+    if (dtype == 1) return TP == 128 ? launch_step_t<PrecBF16, 128>(a, lds, n_tiles, s) : launch_step_t<PrecBF16, 64>(a, lds, n_tiles, s);
+    return TP == 128 ? launch_step_t<PrecF32, 128>(a, lds, n_tiles, s) : launch_step_t<PrecF32, 64>(a, lds, n_tiles, s);
+}
+
+hipError_t marf_launch_loss_final(const double* part, int n, float* out, const float* denom_override, hipStream_t s) {
+    hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(256), 0, s, part, n, out, denom_override);
+    return hipGetLastError();
+}

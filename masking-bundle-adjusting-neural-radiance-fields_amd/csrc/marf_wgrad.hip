@@ -256,11 +256,12 @@ __global__ __launch_bounds__(256) void k_wgrad_last(const float* __restrict__ gl
 }
 
 // Fixed-order sum of the chunk partials into the flat fp32 gradient (nn.Linear layout [M][K],
-// unpadded [Mo][Ko]), then the bias.  Block = 64 outputs x 4 chunk groups; group g sums chunks
+// unpadded [Mo][Ko]), then the bias, optionally times gscale / denom (device scalars).  Block = 64 outputs x 4 chunk groups; group g sums chunks
 // [g*n/4, (g+1)*n/4) with independent loads in flight, the 4 group sums are added in order.
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ partial,
                                                       const float* __restrict__ bpartial, int n_chunks, int M, int K,
-                                                      int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db) {
+                                                      int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db,
+                                                      const float* __restrict__ gscale, const float* __restrict__ denom) {
     __shared__ float red[4][64];
     const long long n = (long long)Mo * Ko;
     const long long e = blockIdx.x * 64LL + (threadIdx.x & 63);
@@ -290,7 +291,9 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
     red[g][threadIdx.x & 63] = s;
     __syncthreads();
     if (g == 0 && e < n + Mo) {
-        const float t = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+        float t = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+        // fused step: the partials carry the unit-upstream gradient without 1/denominator
+        if (gscale) t = t * (gscale[0] / denom[0]);
         if (e < n) dW[e] = t;
         else db[e - n] = t;
     }
@@ -364,9 +367,11 @@ hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* fea
 }
 
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
-                                    int Ko, float* dW, float* db, hipStream_t s) {
+                                    int Ko, float* dW, float* db, hipStream_t s, const float* gscale,
+                                    const float* denom) {
     long long n = (long long)Mo * Ko + Mo;
     int blocks = (int)((n + 63) / 64);
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, s, partial, bpartial, n_chunks, M, K, Mo, Ko, dW, db);
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, s, partial, bpartial, n_chunks, M, K, Mo, Ko, dW, db,
+                       gscale, denom);
     return hipGetLastError();
 }

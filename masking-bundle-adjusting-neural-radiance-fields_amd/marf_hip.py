@@ -46,6 +46,11 @@ _SIGS = {
     "marf_forward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_backward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_vp, _c_vp, _c_int, _c_vp,
                                _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "marf_step_saved_bytes": (_c_sz, [_c_vp, ctypes.POINTER(Geometry)]),
+    "marf_step_forward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_vp, _c_vp, _c_vp, _c_vp,
+                                   _c_vp, _c_vp, _c_vp, _c_vp]),
+    "marf_step_backward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
+                                    _c_vp]),
     "marf_mse_workspace_bytes": (_c_sz, []),
     "marf_masked_mse": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_masked_mse_backward": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
@@ -255,17 +260,24 @@ def coords_geometry(coords):
 
 
 class _Buffers:
-    """Per-device cache of the byte buffers the library borrows (reused across steps)."""
+    """Per-device cache of the byte buffers the library borrows (reused across steps).  Every get()
+    bumps the buffer's generation, so a backward can check that no later forward reused it."""
 
     def __init__(self):
         self.bufs = {}
+        self.gen = {}
 
     def get(self, name, nbytes, device):
-        t = self.bufs.get(name)
-        if t is None or t.numel() < nbytes or t.device != device:
+        key = (name, str(device))
+        t = self.bufs.get(key)
+        if t is None or t.numel() < nbytes:
             t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
-            self.bufs[name] = t
+            self.bufs[key] = t
+        self.gen[key] = self.gen.get(key, 0) + 1
         return t
+
+    def generation(self, name, device):
+        return self.gen.get((name, str(device)), 0)
 
 
 _BUFS = _Buffers()
@@ -377,6 +389,89 @@ class _PlanarRenderFunction(torch.autograd.Function):
         return (dw, None, None, None, None, *grads)
 
 
+class _PlanarStepFunction(torch.autograd.Function):
+    """Graph.forward + Graph.mse_loss of a training step (model/planar.py:329-336, 382-391), fused:
+    the target and mask are known when the forward runs, so marf_step_forward runs the forward, the
+    masked MSE and the whole backward with a unit upstream gradient in one pass over the pixels,
+    and backward() only scales and reduces (marf_step_backward) by the d loss it receives.
+    Outputs: rgb [Bl, Np, 3] and loss_rgb (0-d).  If rgb itself receives a gradient (a caller
+    differentiating through the prediction other than via this loss), backward falls back to the
+    general forward-with-saving + backward path for that part."""
+
+    @staticmethod
+    def forward(ctx, warp_weight, progress, engine, b0, b1, gt, mask, denom_override, *params):
+        ctx.set_materialize_grads(False)
+        w = _f32(warp_weight, "warp_param")
+        Bl = b1 - b0
+        h_local = w[b0:b1].contiguous()
+        Hm = torch.empty(Bl, 3, 3, device=w.device, dtype=torch.float32)
+        st = _stream(w)
+        _check(lib().marf_sl3_to_SL3(_ptr(h_local), _ptr(Hm), Bl, engine.lie_batch(w.shape[0]), st))
+        geo = engine.grid_geo(Bl, Hm)
+        Np = geo_np(engine)
+        gt = _f32(gt, "labels").reshape(Bl, 3, Np)
+        mask = None if mask is None else _f32(mask, "masks").reshape(Bl, 1, Np)
+        rgb = torch.empty(Bl, Np, 3, device=w.device, dtype=torch.float32)
+        stats = torch.empty(3, device=w.device, dtype=torch.float32)
+        packed = engine.packed_for(params)
+        saved = _BUFS.get("planar_step", lib().marf_step_saved_bytes(engine.net.handle, ctypes.byref(geo)), w.device)
+        cf = make_c2f(progress, engine.c2f)
+        _check(lib().marf_step_forward(engine.net.handle, ctypes.byref(geo), ctypes.byref(cf), _ptr(packed), _ptr(gt),
+                                       _ptr(mask), _ptr(denom_override), _ptr(rgb), _ptr(stats), _ptr(saved), st))
+        ctx.save_for_backward(w, progress, rgb, stats)
+        ctx.Hm, ctx.h_local, ctx.saved_buf, ctx.packed, ctx.engine = Hm, h_local, saved, packed, engine
+        ctx.gen = _BUFS.generation("planar_step", w.device)
+        ctx.gt, ctx.mask = gt, mask
+        ctx.b0, ctx.b1 = b0, b1
+        ctx.params = params
+        ctx.shapes = [p.shape for p in params]
+        engine.last_stats = stats  # [loss, denominator, local 3*sum(mask)]
+        return rgb, stats[0]
+
+    @staticmethod
+    def backward(ctx, d_rgb, d_loss):
+        w, progress, rgb, stats = ctx.saved_tensors
+        engine = ctx.engine
+        n_in = 8 + len(ctx.shapes)
+        if d_rgb is None and d_loss is None:
+            return (None,) * n_in
+        if ctx.gen != _BUFS.generation("planar_step", w.device):
+            raise RuntimeError("libmarf: the fused step's saved buffers were reused by a later forward; "
+                               "call backward() before the next Graph.forward")
+        Bl = ctx.b1 - ctx.b0
+        geo = engine.grid_geo(Bl, ctx.Hm)
+        alloc = torch.empty if d_loss is not None else torch.zeros  # the step backward writes every element
+        dflat = alloc(engine.net.param_count, device=w.device, dtype=torch.float32)
+        dh_local = alloc(Bl, 8, device=w.device, dtype=torch.float32)
+        if d_loss is not None:
+            gout = _f32(d_loss.reshape(1).to(torch.float32), "grad")
+            _check(lib().marf_step_backward(engine.net.handle, ctypes.byref(geo), _ptr(ctx.saved_buf), _ptr(ctx.h_local),
+                                            engine.lie_batch(w.shape[0]), _ptr(gout), _ptr(stats), _ptr(dflat),
+                                            _ptr(dh_local), _stream(w)))
+        if d_rgb is not None:
+            # gradient reaching the prediction directly: general path (forward with saving + backward)
+            with torch.enable_grad():
+                wd = w.detach().requires_grad_()
+                ps = [q.detach().requires_grad_() for q in ctx.params]
+                r = _PlanarRenderFunction.apply(wd, progress, engine, ctx.b0, ctx.b1, *ps)
+                gs = torch.autograd.grad(r, [wd] + ps, d_rgb)
+            dh_local = dh_local + gs[0][ctx.b0:ctx.b1]
+            dflat = dflat + torch.cat([g.reshape(-1) for g in gs[1:]])
+        engine.last_flat_grad = dflat
+        if Bl == w.shape[0]:
+            dw = dh_local
+        else:
+            dw = torch.zeros_like(w)
+            dw[ctx.b0:ctx.b1] = dh_local
+        grads = _split_grads(dflat, ctx.shapes)
+        return (dw, None, None, None, None, None, None, None, *grads)
+
+
+def render_step(warp_weight, progress, engine, params, gt, mask, denom_override=None, b0=0, b1=None):
+    b1 = warp_weight.shape[0] if b1 is None else b1
+    return _PlanarStepFunction.apply(warp_weight, progress, engine, b0, b1, gt, mask, denom_override, *params)
+
+
 def geo_np(engine):
     h = (engine.H // 2 + engine.patch_H // 2) - (engine.H // 2 - engine.patch_H // 2)
     w = (engine.W // 2 + engine.patch_W // 2) - (engine.W // 2 - engine.patch_W // 2)
@@ -394,6 +489,7 @@ class Engine:
         self._packed = None
         self._packed_version = None
         self.last_flat_grad = None
+        self.last_stats = None
 
     def lie_batch(self, B):
         return self._lie_batch if self._lie_batch > 0 else B

@@ -312,7 +312,18 @@ class Graph(torch.nn.Module):
 
     def forward(self, var, mode=None):
         b0, b1 = self._range()
-        rgb = self.neural_image.render(self.warp_param.weight, b0, b1)  # [Bl, h*w, 3]
+        imgs = var.get("images")
+        var.fused_loss = None
+        if (torch.is_grad_enabled() and self.opt.get("fused_step", True) and imgs is not None
+                and imgs.get("rgb") is not None and self.opt.loss_weight.render is not None):
+            # training forward: the target is known, so the loss and the whole backward are
+            # computed in the same pass (marf_step_forward); compute_loss picks the loss up
+            masks = imgs.masks[b0:b1] if imgs.get("masks") is not None else None
+            denom = self.loss_denominator if (self.shard is not None and masks is not None) else None
+            rgb, loss_rgb = self.neural_image.render_step(self.warp_param.weight, imgs.rgb[b0:b1], masks, denom, b0, b1)
+            var.fused_loss = (loss_rgb, imgs.rgb, imgs.get("masks"))
+        else:
+            rgb = self.neural_image.render(self.warp_param.weight, b0, b1)  # [Bl, h*w, 3]
         var.rgb_prediction = rgb
         var.rgb_prediction_map = rgb.view(b1 - b0, int(self.h), int(self.w), 3).permute(0, 3, 1, 2)
         if self.opt.use_edges and self.need_edges:
@@ -329,7 +340,11 @@ class Graph(torch.nn.Module):
         imgs = var.images
         if self.opt.loss_weight.render is not None:
             masks = imgs.masks[b0:b1] if imgs.get("masks") is not None else None
-            rgb_loss = self.mse_loss(var.rgb_prediction_map, imgs.rgb[b0:b1], masks)
+            fused = var.get("fused_loss")
+            if fused is not None and fused[1] is imgs.rgb and fused[2] is imgs.get("masks"):
+                rgb_loss = fused[0]  # from the fused training forward (same prediction, target, mask)
+            else:
+                rgb_loss = self.mse_loss(var.rgb_prediction_map, imgs.rgb[b0:b1], masks)
             if self.opt.use_edges:
                 if var.get("edge_prediction") is not None and imgs.get("edges") is not None:
                     me = imgs.masks_eroded[b0:b1] if imgs.get("masks_eroded") is not None else None
@@ -429,6 +444,13 @@ class NeuralImageFunction(torch.nn.Module):
         """Fused training forward over the crop pixels of patches [b0, b1)."""
         ps = self._params()
         return marf_hip.render_train(warp_weight, self.progress.detach(), self.engine(warp_weight.device), ps, b0, b1)
+
+    def render_step(self, warp_weight, gt, masks, denom=None, b0=0, b1=None):
+        """Fused training forward + masked MSE (+ the backward of both, applied when the loss is
+        differentiated): returns (rgb [Bl, h*w, 3], loss_rgb)."""
+        ps = self._params()
+        return marf_hip.render_step(warp_weight, self.progress.detach(), self.engine(warp_weight.device), ps, gt, masks,
+                                    denom, b0, b1)
 
     def forward(self, coord_2d):
         """rgb = MLP(cat[coord, posenc(coord)]) for explicit coordinates [..., 2] (:429-449)."""

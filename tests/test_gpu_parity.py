@@ -385,3 +385,96 @@ def test_shard_gradients_match_single(tmp_path):
     np.testing.assert_allclose(a[2] + b[2], full[2], rtol=1e-6)
     assert torch.allclose(a[1][:2] + b[1][:2], full[1][:2], atol=1e-6 * full[1].abs().max())
     assert torch.allclose(b[1][2:], full[1][2:], atol=1e-6 * full[1].abs().max())
+
+
+# ------------------------------------------------------------------------ fused training step
+
+def _grads_of(m):
+    return ([p.grad.detach().clone() for p in m.graph.neural_image.mlp.parameters()],
+            m.graph.warp_param.weight.grad.detach().clone())
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("tag", ["a", "c"])
+def test_fused_step_matches_separate_kernels(tag, precision, tmp_path):
+    """marf_step_forward/backward (forward + loss + backward in one pass per tile) against the
+    separate forward / masked-MSE / backward kernels on the same state."""
+    res = []
+    for fused in (True, False):
+        z, m, var, nl = small_setup(tag, precision, tmp_path)
+        m.opt.fused_step = fused
+        var, loss = one_step_grads(m, var)
+        assert (var.fused_loss is not None) == fused
+        res.append((var.rgb_prediction.detach().clone(), float(loss.rgb), *_grads_of(m)))
+    (rf, lf, gf, wf), (ru, lu, gu, wu) = res
+    assert torch.equal(rf, ru)  # same forward arithmetic
+    np.testing.assert_allclose(lf, lu, rtol=1e-6)
+    for a, b in zip(gf, gu):
+        if precision == "fp32":
+            assert (a - b).abs().max() <= 1e-5 * b.abs().max() + 1e-12
+        else:  # the fused last-layer weight gradient multiplies bf16(g) instead of fp32 g
+            cos = float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
+            assert cos > 0.999 and (a - b).abs().max() <= 2e-2 * b.abs().max() + 1e-12
+    tol = 1e-5 if precision == "fp32" else 2e-2
+    assert (wf - wu).abs().max() <= tol * wu.abs().max() + 1e-12
+
+
+def test_fused_step_gradient_through_prediction(tmp_path):
+    """A second loss term on the prediction itself: the fused function falls back to the general
+    path for that part; the result equals the separate-kernel path (fp32, <= 1e-5 rel)."""
+    res = []
+    for fused in (True, False):
+        z, m, var, nl = small_setup("a", "fp32", tmp_path)
+        m.opt.fused_step = fused
+        m.optim.zero_grad()
+        var = m.graph.forward(var, mode="train")
+        loss = m.summarize_loss(m.graph.compute_loss(var, mode="train"))
+        (loss.all + 0.1 * (var.rgb_prediction ** 2).mean()).backward()
+        res.append(_grads_of(m))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert (a - b).abs().max() <= 1e-5 * b.abs().max() + 1e-12
+    assert (res[0][1] - res[1][1]).abs().max() <= 1e-5 * res[1][1].abs().max() + 1e-12
+
+
+def test_fused_step_stale_buffer_raises(tmp_path):
+    z, m, var, nl = small_setup("a", "fp32", tmp_path)
+    v1 = m.graph.forward(var, mode="train")
+    l1 = m.graph.compute_loss(v1, mode="train").rgb
+    m.graph.forward(var, mode="train")  # reuses the saved buffers
+    with pytest.raises(RuntimeError, match="reused"):
+        l1.backward()
+
+
+def test_fused_step_c3_linearity_and_determinism(tmp_path):
+    """C3 geometry through the fused loss path: bit-identical reruns, d loss x2 -> gradients x2."""
+    from model import planar
+    from util import EasyDict as edict
+    B = 4
+    opt = make_opt(tmp_path, H=512, W=512, patch_H=256, patch_W=256, batch_size=B, precision="bf16",
+                   arch={"layers": [None, 256, 256, 256, 256, 3], "skip": [], "posenc": {"L_2D": 16}})
+    torch.manual_seed(0)
+    graph = planar.Graph(opt).to(DEV)
+    graph.neural_image.progress.data.fill_(0.2)
+    rng = np.random.default_rng(2)
+    gt = t(rng.random((B, 3, 256, 256)).astype(np.float32))
+    mask = t((rng.random((B, 1, 256, 256)) < 0.85).astype(np.float32))
+    var = edict(images=edict(rgb=gt, masks=mask, masks_eroded=mask, edges=None))
+    graph.need_edges = False
+    with torch.no_grad():
+        graph.warp_param.weight.copy_(t((rng.standard_normal((B, 8)) * 0.01).astype(np.float32)))
+
+    def run(scale):
+        for p in graph.parameters():
+            p.grad = None
+        v = graph.forward(var)
+        loss = graph.compute_loss(v).rgb
+        (loss * scale).backward()
+        return float(loss), [p.grad.clone() for p in graph.neural_image.mlp.parameters()], graph.warp_param.weight.grad.clone()
+
+    l1, g1, w1 = run(1.0)
+    l2, g2, w2 = run(1.0)
+    l3, g3, w3 = run(2.0)
+    assert l1 == l2 == l3
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2)) and torch.equal(w1, w2)
+    assert all(torch.equal(2 * a, b) for a, b in zip(g1, g3)) and torch.equal(2 * w1, w3)
+    assert all(torch.isfinite(a).all() for a in g1) and torch.isfinite(w1).all()
