@@ -38,6 +38,59 @@ MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int col
     }
 }
 
+// Streams an LDS tile [rows][lda] (first `cols` columns) to global [rows][ldd] in 16-byte chunks,
+// `per` chunks per issue() call.  gemm_rows calls issue() once per k-step, so a layer's saved
+// activations leave while the next GEMM (which reads the same tile) runs: stores issued as one
+// burst in front of the GEMM would sit ahead of its weight loads in the in-order vmcnt queue and
+// stall the first MFMA until the whole burst has drained.  bf16 tiles only (16-B aligned rows).
+template <class T>
+struct TileStore {
+    // Wave-uniform walk: one issue = one 16-B chunk per lane covering rpi = 64 / nch whole rows
+    // (lane -> row lane / nch, chunk lane % nch); wave w copies row groups w, w + 4, ...  The
+    // source is the LDS tile the GEMM reads (passed to issue()); an idle job has q == nq.
+    T* dst;
+    int lda, ldd, rows, rpi, q, nq, per, wave;
+    int lr, lc;  // per lane
+
+    MARF_DEV void clear() {
+        q = nq = 0;
+        per = 0;
+    }
+    MARF_DEV void init(int lda_, T* d, int ldd_, int rows_, int cols, int nk, int wave_, int lane) {
+        constexpr int VEC = 16 / sizeof(T);
+        const int nch = cols / VEC;  // <= 64 (cols <= 512)
+        dst = d;
+        lda = lda_;
+        ldd = ldd_;
+        rows = rows_;
+        wave = wave_;
+        rpi = 64 / nch;
+        lr = lane / nch;
+        lc = lane - lr * nch;
+        if (lr >= rpi) lr = 1 << 20;  // idle lane (64 % nch)
+        q = 0;
+        nq = (rows + 4 * rpi - 1) / (4 * rpi);
+        per = (nq + nk - 1) / nk;
+    }
+    MARF_DEV void one(const T* src) {
+        constexpr int VEC = 16 / sizeof(T);
+        if (q < nq) {
+            const int r = (q * 4 + wave) * rpi + lr;
+            if (r < rows) {
+                const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)r * lda + VEC * lc);
+                *reinterpret_cast<uint4*>(dst + (size_t)r * ldd + VEC * lc) = v;
+            }
+            ++q;
+        }
+    }
+    MARF_DEV void issue(const T* src) {
+        for (int u = 0; u < per; ++u) one(src);
+    }
+    MARF_DEV void flush(const T* src) {
+        while (q < nq) one(src);
+    }
+};
+
 // acc[i][PT] += W[rows (wave + 4 i)*32 .., k] . act[px, k]^T over k < K for the NA row tiles this
 // wave owns (i < NA).  NA is dispatched once per layer (wave-uniform), so the body is branch-free.
 //
@@ -47,7 +100,7 @@ MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int col
 // statically named buffers).  Loads past the last k-step are clamped to it (harmless L2 hits).
 template <class P, int NA, int RT, int PT>
 MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__ W, int K,
-                        const typename P::T* act, int lda, int wave, int lane) {
+                        const typename P::T* act, int lda, int wave, int lane, TileStore<typename P::T>& st) {
     typedef typename P::frag F;
     const int ko = P::kofs(lane);
     const int rl = lane & 31;
@@ -86,12 +139,15 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
             __builtin_amdgcn_sched_barrier(0);
             ldA(A0, k + 2);
             ldB(B0, k + 2);
+            st.issue(act);
             __builtin_amdgcn_sched_barrier(0);
             mma(A1, B1);
             __builtin_amdgcn_sched_barrier(0);
             ldA(A1, k + 3);
+            st.issue(act);
         }
         if (k < nk) mma(A0, B0);
+        st.flush(act);
         return;
     }
     ldA(A0, 0);
@@ -109,20 +165,24 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
         __builtin_amdgcn_sched_barrier(0);
         ldA(A0, k + 4);
         ldB(B0, k + 2);
+        st.issue(act);
         __builtin_amdgcn_sched_barrier(0);
         mma(A1, B1);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A1, k + 5);
         ldB(B1, k + 3);
+        st.issue(act);
         __builtin_amdgcn_sched_barrier(0);
         mma(A2, B0);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A2, k + 6);
         ldB(B0, k + 4);
+        st.issue(act);
         __builtin_amdgcn_sched_barrier(0);
         mma(A3, B1);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A3, k + 7);
+        st.issue(act);
     }
     // remainder (nk % 4 steps): A0..A2 hold steps k..k+2, B0 holds step k
     if (k < nk) {
@@ -134,13 +194,15 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
             if (k + 2 < nk) mma(A2, B0);
         }
     }
+    st.flush(act);
 }
 
 // Accumulators start at the bias of their output row when `bias` is given (so the epilogue does
 // not add it), else at zero.
 template <class P, int RT, int PT>
 MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__ W, int K, int n_rt,
-                        const typename P::T* act, int lda, int wave, int lane, const float* bias = nullptr) {
+                        const typename P::T* act, int lda, int wave, int lane, const float* bias,
+                        TileStore<typename P::T>& st) {
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
         f32x16 init = (f32x16){};
@@ -162,11 +224,11 @@ MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
     int na = (n_rt - wave + 3) / 4;
     na = na < 0 ? 0 : (na > RT ? RT : na);
     switch (na) {
-        case 1: gemm_rows<P, 1, RT, PT>(acc, W, K, act, lda, wave, lane); break;
-        case 2: gemm_rows<P, 2, RT, PT>(acc, W, K, act, lda, wave, lane); break;
-        case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT>(acc, W, K, act, lda, wave, lane); break;
-        case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT>(acc, W, K, act, lda, wave, lane); break;
-        default: break;
+        case 1: gemm_rows<P, 1, RT, PT>(acc, W, K, act, lda, wave, lane, st); break;
+        case 2: gemm_rows<P, 2, RT, PT>(acc, W, K, act, lda, wave, lane, st); break;
+        case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT>(acc, W, K, act, lda, wave, lane, st); break;
+        case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT>(acc, W, K, act, lda, wave, lane, st); break;
+        default: st.flush(act); break;
     }
 }
 
@@ -196,6 +258,20 @@ MARF_DEV void tile_origin(const GeoDev& g, int tile, int TP, int& b, int& p0, lo
     slot0 = (long long)b * g.Np_pad + p0;
 }
 
+
+// Save the LDS tile to global: bf16 tiles stream during the GEMM that follows (job handed to
+// gemm_tile), fp32 tiles (unaligned LDS rows) are copied right away (job left idle).
+template <class P>
+MARF_DEV void save_tile(TileStore<typename P::T>& job, const typename P::T* act, int lda, int rows, int cols,
+                        typename P::T* dst, int nk_next) {
+    if constexpr (sizeof(typename P::T) == 2) {
+        const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        job.init(lda, dst, cols, rows, cols, nk_next > 0 ? nk_next : 1, wave, lane);
+    } else {
+        copy_tile_out<P>(act, lda, rows, cols, dst, cols);
+        job.clear();
+    }
+}
 
 // ======================================================================== per-tile phases
 
@@ -325,7 +401,7 @@ MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
 template <class P, int TP>
 MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh, char* smem, int lda,
                            int wave, int lane, int b, int p0, float* red, float* red9, float* dH_partial,
-                           float* d_coords) {
+                           float* d_coords, TileStore<typename P::T>& st) {
     typedef typename P::T T;
     constexpr int PT = TP / 32;
     constexpr int RT = 8 / PT;
@@ -333,7 +409,7 @@ MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, con
     const T* act = reinterpret_cast<const T*>(smem);
     const int R = net.Kp[0], Kk = net.Mt[0], n_rt = R / 32;
     f32x16 acc[RT][PT];
-    gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[0]), Kk, n_rt, act, lda, wave, lane);
+    gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[0]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
     __syncthreads();
     float* df = reinterpret_cast<float*>(smem);
     const int ldf = R + 1;

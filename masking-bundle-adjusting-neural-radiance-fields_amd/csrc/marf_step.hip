@@ -57,18 +57,21 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     __syncthreads();
     tile_prologue<P, TP>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0);
     __syncthreads();
-    copy_tile_out<P>(act, lda, TP, net.Kp[0], reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0]);
+    // every saved tile streams out during the GEMM that reads it next (TileStore)
+    TileStore<T> st;
+    save_tile<P>(st, act, lda, TP, net.Kp[0], reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0] / P::KS);
 
     // ---- hidden layers (forward)
     for (int l = 0; l < nl - 1; ++l) {
         const int K = net.Kp[l], M = net.Mp[l], n_rt = M / 32;
         f32x16 acc[RT][PT];
-        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l]);
+        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l], st);
         __syncthreads();  // every wave has consumed the layer input
         relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], slot0);
         __syncthreads();
+        st.clear();
         if (l + 1 < nl - 1)  // the last layer's input never leaves LDS
-            copy_tile_out<P>(act, lda, TP, M, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M);
+            save_tile<P>(st, act, lda, TP, M, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M / P::KS);
     }
 
     // ---- last layer (3 outputs, rows padded to 16): 16x16 MFMA, TP/4 pixels per wave, sigmoid,
@@ -203,18 +206,19 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     __syncthreads();
 
     // ---- dgrad chain, l = n-1 .. 1 : dfeat_l = W_l^T dz_{l+1}; dz_l = dfeat_l * relu'(feat_l)
+    st.clear();
     for (int l = nl - 1; l >= 1; --l) {
         const int R = net.Kp[l], Kk = net.Mt[l], n_rt = R / 32;
         f32x16 acc[RT][PT];
-        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane);
+        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
         __syncthreads();
         mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l], slot0);
         __syncthreads();
-        copy_tile_out<P>(act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, R);
+        save_tile<P>(st, act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, net.Mt[l - 1] / P::KS);
     }
 
     // ---- layer-0 dgrad + posenc / warp adjoint -> dH partial
-    warp_adjoint<P, TP>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr);
+    warp_adjoint<P, TP>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st);
 }
 
 // Loss of the fused step from the per-tile partials (fp64, fixed-order tree):
