@@ -12,6 +12,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "lib", "libmarf.so")
+# diagnostic variant with in-kernel phase stamps (tools/phase_stamps.py); never loaded by default
+LIB_STAMPS = os.path.join(HERE, "lib", "libmarf_stamps.so")
 SOURCES = ["marf_lie.hip", "marf_mlp.hip", "marf_wgrad.hip", "marf_step.hip", "marf_misc.hip", "marf_abi.hip", "marf_prof.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          # exact fp32 operation order for the bit-exact prologue (no implicit FMA contraction)
@@ -26,21 +28,27 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
+def build(force=False, verbose=True, stamps=False):
+    if stamps:
+        return _compile(LIB_STAMPS, ["-DMARF_STAMPS"], verbose)
     if not force and not _stale():
         return LIB
+    return _compile(LIB, [], verbose)
+
+
+def _compile(lib_path, extra, verbose):
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    tmp = LIB + ".tmp"
-    cmd = [hipcc] + FLAGS + [os.path.join(HERE, "csrc", s) for s in SOURCES] + ["-o", tmp]
+    os.makedirs(os.path.dirname(lib_path), exist_ok=True)
+    tmp = lib_path + ".tmp"
+    cmd = [hipcc] + FLAGS + extra + [os.path.join(HERE, "csrc", s) for s in SOURCES] + ["-o", tmp]
     if verbose:
-        print("[marf] building", LIB, flush=True)
+        print("[marf] building", lib_path, flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, stamps="--stamps" in sys.argv)

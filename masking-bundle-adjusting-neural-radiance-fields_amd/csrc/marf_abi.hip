@@ -17,6 +17,7 @@
 using namespace marf;
 
 static thread_local std::string g_err;
+static unsigned long long* g_stamps = nullptr;  // diagnostic phase stamps (MARF_STAMPS builds)
 
 static int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -56,6 +57,9 @@ struct marf_net {
 extern "C" {
 
 const char* marf_last_error(void) { return g_err.c_str(); }
+
+// Diagnostic builds only: device buffer [n_tiles][16] for the fused step's phase stamps.
+void marf_debug_set_stamps(void* d_stamps) { g_stamps = (unsigned long long*)d_stamps; }
 int marf_version(void) { return 1; }
 
 // ------------------------------------------------------------------ Lie / warp / posenc
@@ -551,6 +555,7 @@ int marf_step_forward(const marf_net* net, const marf_geometry* geo, const marf_
     a.blast_partial = (float*)(sv + p.blast);
     a.dH_partial = (float*)(sv + p.dH);
     a.loss_partial = (double*)(sv + p.loss);
+    a.stamps = g_stamps;
     {
         MarfProfScope ps("mlp_step", s);
         HIPCHK(marf_launch_mlp_step(a, net->dtype, net->TP, net->lds_step, p.n_tiles, s), "step_forward");

@@ -52,6 +52,7 @@ struct StepArgs {
     float* blast_partial;                   // out: [n_tiles][3]
     float* dH_partial;                      // out: [n_tiles][9]
     double* loss_partial;                   // out: [n_tiles][2] = sum ((p - g) m)^2, sum m
+    unsigned long long* stamps;             // diagnostic builds (MARF_STAMPS): [n_tiles][16] s_memtime
     long long S;
     int lda;
 };

@@ -8,8 +8,13 @@
 //   * relu masks         mask_l : uint64 [S/32][Kp_l/32][16]: for pixel tile p (32 slots), row tile t and
 //                        accumulator register r, bit `lane` = (feature 32t + acc_row(lane, r) of
 //                        slot 32p + (lane & 31)) > 0 -- the wave ballot of that register.
-//   * packed weights     Wf_l   : [Mp_l][Kp_l] T (forward A operand, nn.Linear row layout, zero pad)
-//                        Wt_l   : [Kp_l][Mt_l] T (transposed, backward A operand)
+//   * packed weights     Wf_l   : W_l [Mp_l][Kp_l] (forward A operand, zero padded) and
+//                        Wt_l   : W_l^T [Kp_l][Mt_l] (backward A operand), both FRAGMENT-MAJOR: for
+//                        row tile rt and k-step ks the 64 lanes' MFMA A fragments are one
+//                        contiguous 64 * FE-element block at ((rt * nk + ks) * 64 + lane) * FE,
+//                        so a wave's weight load is one fully used 1 KB (bf16) burst.  Lane l of
+//                        a 32x32 fragment holds row 32 rt + (l & 31), k = ks KS + (l >> 5) FE + j;
+//                        the 16-row last layer (16x16 MFMA) row l & 15, k = ks KS16 + (l >> 4) FE + j.
 //   * MFMA 32x32 accumulator map (both dtypes): lane l, reg r -> col = l&31,
 //     row = (r&3) + 8*(r>>2) + 4*(l>>5).
 #pragma once
@@ -44,6 +49,7 @@ struct PrecBF16 {
     typedef u16 T;
     static constexpr int KS = 16;       // k per MFMA (32x32 shape)
     static constexpr int KS16 = 32;     // k per MFMA (16x16 shape)
+    static constexpr int FE = 8;        // elements per lane per A/B fragment
     typedef bf16x8 frag;
     static constexpr int kDtype = 1;
 
@@ -68,6 +74,7 @@ struct PrecF32 {
     typedef float T;
     static constexpr int KS = 2;
     static constexpr int KS16 = 4;
+    static constexpr int FE = 1;
     typedef float frag;
     static constexpr int kDtype = 0;
 

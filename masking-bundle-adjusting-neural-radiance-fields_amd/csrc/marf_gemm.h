@@ -105,12 +105,13 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
     const int ko = P::kofs(lane);
     const int rl = lane & 31;
     const int nk = K / P::KS;
+    // fragment-major weights (marf_common.h): fragment (rt, ks) at ((rt * nk + ks) * 64 + lane) * FE
     const typename P::T* wrow[NA];
 #pragma unroll
-    for (int i = 0; i < NA; ++i) wrow[i] = W + (size_t)((wave + 4 * i) * 32 + rl) * K + ko;
+    for (int i = 0; i < NA; ++i) wrow[i] = W + ((size_t)(wave + 4 * i) * nk * 64 + lane) * P::FE;
     const typename P::T* brow = act + (size_t)rl * lda + ko;
     auto ldA = [&](F (&dst)[NA], int k) {
-        const int kc = (k < nk ? k : nk - 1) * P::KS;
+        const int kc = (k < nk ? k : nk - 1) * 64 * P::FE;
 #pragma unroll
         for (int i = 0; i < NA; ++i) dst[i] = P::load_frag(wrow[i] + kc);
     };

@@ -115,6 +115,26 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
 
 // ------------------------------------------------------------------ packing
 
+// Fragment-major packing (layout: marf_common.h).  Element e of a packed matrix with R rows (tiles
+// of TR = 32 or 16 rows) and Kp columns: j = e % FE, lane, ks, rt from the rest; (row, k) from the
+// MFMA fragment map of the tile shape.  src(row, k) = W[row][k] (forward) or W[k][row] (transposed).
+template <class P>
+MARF_DEV void frag_coord(long long e, int nk, bool t16, int& row, int& k) {
+    const int j = (int)(e % P::FE);
+    long long r = e / P::FE;
+    const int lane = (int)(r % 64);
+    r /= 64;
+    const int ks = (int)(r % nk);
+    const int rt = (int)(r / nk);
+    if (t16) {
+        row = rt * 16 + (lane & 15);
+        k = ks * P::KS16 + (lane >> 4) * P::FE + j;
+    } else {
+        row = rt * 32 + (lane & 31);
+        k = ks * P::KS + (lane >> 5) * P::FE + j;
+    }
+}
+
 template <class P>
 __global__ void k_pack(const float* __restrict__ params, char* __restrict__ packed, PackArgs a) {
     typedef typename P::T T;
@@ -127,14 +147,17 @@ __global__ void k_pack(const float* __restrict__ params, char* __restrict__ pack
     const float* bsrc = params + L.b_off;
     const long long nf = (long long)L.Mp * L.Kp;
     const long long nt = (long long)L.Kp * L.Mt;
+    const bool last16 = L.Mp == 16;  // the 3-output layer runs on 16x16 MFMA
+    const int nkf = L.Kp / (last16 ? P::KS16 : P::KS), nkt = L.Mt / P::KS;
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < nf + nt + L.Mp; e += (long long)gridDim.x * 256) {
         if (e < nf) {
-            int m = (int)(e / L.Kp), k = (int)(e % L.Kp);
+            int m, k;
+            frag_coord<P>(e, nkf, last16, m, k);
             wf[e] = P::cvt(m < L.M && k < L.K ? W[(size_t)m * L.K + k] : 0.f);
         } else if (e < nf + nt) {
-            long long f = e - nf;
-            int k = (int)(f / L.Mt), m = (int)(f % L.Mt);
-            wt[f] = P::cvt(m < L.M && k < L.K ? W[(size_t)m * L.K + k] : 0.f);
+            int kr, m;  // row of W^T = input feature, column = output feature
+            frag_coord<P>(e - nf, nkt, false, kr, m);
+            wt[e - nf] = P::cvt(m < L.M && kr < L.K ? W[(size_t)m * L.K + kr] : 0.f);
         } else {
             int m = (int)(e - nf - nt);
             bias[m] = m < L.M ? bsrc[m] : 0.f;

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
         for (int j = 0; j < NJ; ++j) acc[j] = (f32x4){};
         const int ko = P::kofs16(lane);
         for (int k0 = 0; k0 < K; k0 += P::KS16) {
-            typename P::frag wa = P::load_frag(W + (size_t)(lane & 15) * K + k0 + ko);
+            typename P::frag wa = P::load_frag(W + ((size_t)(k0 / P::KS16) * 64 + lane) * P::FE);
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int px = wave * (TP / 4) + j * 16 + (lane & 15);

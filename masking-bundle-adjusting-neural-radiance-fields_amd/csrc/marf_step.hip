@@ -30,6 +30,16 @@ MARF_DEV i16x4 tr_read16(const u16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
 }
 
+// Phase timestamps of wave 0 (diagnostic build only: -DMARF_STAMPS, tools/phase_stamps.py).
+#ifdef MARF_STAMPS
+#define STAMP(i)                                                                                   \
+    do {                                                                                           \
+        if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
+
 template <class P, int TP>
 __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     typedef typename P::T T;
@@ -53,10 +63,12 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     const int nl = net.n_layers;
     const int Np = a.geo.Np;
 
+    STAMP(0);
     c2f_weights_lds(a.c2f, net.L, wsh);
     __syncthreads();
     tile_prologue<P, TP>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0);
     __syncthreads();
+    STAMP(1);
     // every saved tile streams out during the GEMM that reads it next (TileStore)
     TileStore<T> st;
     save_tile<P>(st, act, lda, TP, net.Kp[0], reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0] / P::KS);
@@ -67,8 +79,10 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         f32x16 acc[RT][PT];
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l], st);
         __syncthreads();  // every wave has consumed the layer input
+        STAMP(2 + 2 * l);
         relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], slot0);
         __syncthreads();
+        if (l < 3) STAMP(3 + 2 * l);
         st.clear();
         if (l + 1 < nl - 1)  // the last layer's input never leaves LDS
             save_tile<P>(st, act, lda, TP, M, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M / P::KS);
@@ -85,7 +99,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         for (int j = 0; j < NJ; ++j) acc[j] = (f32x4){};
         const int ko = P::kofs16(lane);
         for (int k0 = 0; k0 < Kl; k0 += P::KS16) {
-            typename P::frag wa = P::load_frag(W + (size_t)(lane & 15) * Kl + k0 + ko);
+            typename P::frag wa = P::load_frag(W + ((size_t)(k0 / P::KS16) * 64 + lane) * P::FE);
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int px = wave * (TP / 4) + j * 16 + (lane & 15);
@@ -129,6 +143,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     }
     __syncthreads();
 
+    STAMP(9);
     // ---- masked-MSE partial of the tile (fp64, fixed order) and the last bias gradient
     if (wave == 0) {
         double s0 = 0.0, s1 = 0.0;
@@ -200,6 +215,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         const int Kt = net.Mt[nl - 1];
         for (int c = 0; c < Kt; ++c) row[c] = P::cvt(c < 3 ? gl[i][c] : 0.f);
     }
+    STAMP(10);
     // the ReLU mask records were written by this same wave with vector stores: drain them to L2
     // before the scalar loads of the dgrad epilogues read them back
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -214,11 +230,13 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         __syncthreads();
         mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l], slot0);
         __syncthreads();
+        if (l <= 4) STAMP(15 - l);  // 14 .. 11
         save_tile<P>(st, act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, net.Mt[l - 1] / P::KS);
     }
 
     // ---- layer-0 dgrad + posenc / warp adjoint -> dH partial
     warp_adjoint<P, TP>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st);
+    STAMP(15);
 }
 
 // Loss of the fused step from the per-tile partials (fp64, fixed-order tree):

@@ -11,7 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmarf.so")
+# MARF_LIB selects a diagnostic build (lib/libmarf_stamps.so, tools/phase_stamps.py)
+LIB_PATH = os.environ.get("MARF_LIB") or os.path.join(_HERE, "lib", "libmarf.so")
 
 MARF_FP32, MARF_BF16 = 0, 1
 GEO_GRID, GEO_COORDS = 0, 1
@@ -56,6 +57,7 @@ _SIGS = {
     "marf_masked_mse_backward": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_adam_step": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_ll, _c_dbl, _c_dbl, _c_dbl, _c_dbl, _c_ll, _c_vp,
                                 _c_vp]),
+    "marf_debug_set_stamps": (None, [_c_vp]),
     "marf_profile_enable": (_c_int, [_c_int]),
     "marf_profile_reset": (_c_int, []),
     "marf_profile_read": (_c_int, [ctypes.c_char_p, _c_int, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_ll), _c_int]),
