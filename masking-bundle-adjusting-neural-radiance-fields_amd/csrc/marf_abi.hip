@@ -300,7 +300,7 @@ static void plan_saved(const marf_net* n, long long S, SavedPlan& p) {
     p.mask[0] = 0;
     for (int l = 1; l < n->n_layers; ++l) {
         p.mask[l] = off;
-        off += rup((long long)(n->Kp[l] / 32) * S * 4, 256);
+        off += rup(S / n->TP * 4096, 256);  // mask records: one uint4 per lane per wave per tile
     }
     p.total = off;
 }
@@ -491,7 +491,7 @@ static void plan_step(const marf_net* n, long long S, StepPlan& p) {
         p.dz[l] = off;
         off += rup((long long)S * n->Kp[l] * n->elem, 256);
         p.mask[l] = off;
-        off += rup((long long)(n->Kp[l] / 32) * S * 4, 256);
+        off += rup(S / n->TP * 4096, 256);
     }
     p.wlast = off;
     off += rup((long long)p.n_tiles * 3 * n->Kp[nl - 1] * 4, 256);

@@ -314,13 +314,22 @@ MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, co
     for (int f = net.D + part; f < net.Kp[0]; f += NPART) row[f] = P::cvt(0.f);
 }
 
+// ReLU mask records: one uint4 per lane per (tile, layer) at ((tile * 4 + wave) * 64 + lane), i.e.
+// one contiguous 1 KB wave burst.  The RT x PT accumulator tiles of a wave are numbered
+// ti = i * PT + j (<= 8); tile ti's 16 bits live in word ti >> 1, bits 16 (1 - (ti & 1)) + 15 - r
+// for accumulator register r.  The dgrad epilogue of the backward finds the same (feature, pixel)
+// in the same wave / lane / register (gemm_tile deals row tiles identically for W and W^T).
+MARF_DEV uint4* mask_record(uint64_t* mk, int tile, int wave, int lane) {
+    return reinterpret_cast<uint4*>(mk) + ((size_t)tile * 4 + wave) * 64 + lane;
+}
+
 // Hidden-layer epilogue: ReLU of the accumulators (bias already in them) written back to act in
-// place, and (mk != null) the ReLU masks: per (pixel tile, row tile) 128 contiguous bytes = the 16
-// wave ballots (one per accumulator register), gathered into lanes 0..31 of one VGPR by
-// v_writelane and written with one vector store.
+// place, and (mk != null) the ReLU mask record of this wave.  Per element: v_cmp (vcc = z > 0),
+// v_cndmask (relu), v_addc (shift the bit into the tile's mask word).
 template <class P, int RT, int PT>
 MARF_DEV void relu_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, int n_rt, int wave, int lane,
-                            uint64_t* mk, long long slot0) {
+                            uint64_t* mk, int tile) {
+    uint32_t words[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
         const int rt = wave + 4 * i;
@@ -328,39 +337,37 @@ MARF_DEV void relu_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
         const int rbase = rt * 32 + 4 * (lane >> 5);
 #pragma unroll
         for (int j = 0; j < PT; ++j) {
+            const int ti = i * PT + j;
             const int px = j * 32 + (lane & 31);
             float o[16];
-            uint64_t bal[16];  // the v_cmp results themselves (SGPR pairs)
+            uint32_t bits = 0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float z = acc[i][j][r];
-                const bool pos = z > 0.f;
-                o[r] = pos ? z : 0.f;
-                bal[r] = __ballot(pos);
+                float v;
+                asm volatile(
+                    "v_cmp_lt_f32_e32 vcc, 0, %2\n\t"
+                    "v_cndmask_b32_e32 %0, 0, %2, vcc\n\t"
+                    "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+                    : "=&v"(v), "+v"(bits)
+                    : "v"(acc[i][j][r])
+                    : "vcc");
+                o[r] = v;
             }
+            words[ti >> 1] |= bits << (16 * (1 - (ti & 1)));
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 store4<P>(act + (size_t)px * lda + rbase + 8 * q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-            if (mk) {
-                uint32_t w = 0;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"((uint32_t)bal[r]), "n"(2 * r));
-                    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"((uint32_t)(bal[r] >> 32)), "n"(2 * r + 1));
-                }
-                uint32_t* mrow = reinterpret_cast<uint32_t*>(mk + (((slot0 >> 5) + j) * n_rt + rt) * 16);
-                if (lane < 32) mrow[lane] = w;
-            }
         }
     }
+    if (mk) *mask_record(mk, tile, wave, lane) = make_uint4(words[0], words[1], words[2], words[3]);
 }
 
-// Dgrad epilogue: dz = acc * relu'(feat) with the masks saved by relu_epilogue, written to act.
-// The 16 wave-uniform lane masks of a tile come in with two scalar loads; each element is one
-// v_cndmask.
+// Dgrad epilogue: dz = acc * relu'(feat) with this wave's mask record `mw` (loaded before the GEMM),
+// written to act.  Per element: v_bfe_i32 (0 / -1 from the bit) and v_and.
 template <class P, int RT, int PT>
 MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, int n_rt, int wave, int lane,
-                            const uint64_t* mk, long long slot0) {
+                            uint4 mw) {
+    const uint32_t words[4] = {mw.x, mw.y, mw.z, mw.w};
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
         const int rt = wave + 4 * i;
@@ -368,25 +375,14 @@ MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
         const int rbase = rt * 32 + 4 * (lane >> 5);
 #pragma unroll
         for (int j = 0; j < PT; ++j) {
+            const int ti = i * PT + j;
             const int px = j * 32 + (lane & 31);
-            const uint64_t* mrow = mk + (((slot0 >> 5) + j) * n_rt + rt) * 16;
-            u32x16 m0, m1;
-            asm volatile(
-                "s_load_dwordx16 %0, %2, 0x0\n\t"
-                "s_load_dwordx16 %1, %2, 0x40\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&s"(m0), "=&s"(m1)
-                : "s"(mrow)
-                : "memory");
+            const uint32_t w = words[ti >> 1];
             float o[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const uint32_t lo = r < 8 ? m0[2 * r] : m1[2 * r - 16];
-                const uint32_t hi = r < 8 ? m0[2 * r + 1] : m1[2 * r - 15];
-                const uint64_t ms = ((uint64_t)hi << 32) | lo;
-                float v;
-                asm volatile("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(v) : "v"(acc[i][j][r]), "s"(ms));
-                o[r] = v;
+                const int m = __builtin_amdgcn_sbfe((int)w, 16 * (1 - (ti & 1)) + 15 - r, 1);
+                o[r] = __int_as_float(__float_as_int(acc[i][j][r]) & m);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q)

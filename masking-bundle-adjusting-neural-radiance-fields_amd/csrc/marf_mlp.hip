@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
         f32x16 acc[RT][PT];
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l], st);
         __syncthreads();  // every wave has consumed the layer input
-        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask[l + 1], slot0);
+        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask[l + 1], blockIdx.x);
         __syncthreads();
         st.clear();
         if (a.feat[l + 1]) {
@@ -152,9 +152,10 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(BwdArgs a) {
     for (int l = nl - 1; l >= 1; --l) {
         const int R = net.Kp[l], Kk = net.Mt[l], n_rt = R / 32;
         f32x16 acc[RT][PT];
+        const uint4 mw = *mask_record(const_cast<uint64_t*>(a.mask[l]), blockIdx.x, wave, lane);
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
         __syncthreads();
-        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask[l], slot0);
+        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, mw);
         __syncthreads();
         save_tile<P>(st, act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, net.Mt[l - 1] / P::KS);
     }

@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l], st);
         __syncthreads();  // every wave has consumed the layer input
         STAMP(2 + 2 * l);
-        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], slot0);
+        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x);
         __syncthreads();
         if (l < 3) STAMP(3 + 2 * l);
         st.clear();
@@ -216,9 +216,6 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         for (int c = 0; c < Kt; ++c) row[c] = P::cvt(c < 3 ? gl[i][c] : 0.f);
     }
     STAMP(10);
-    // the ReLU mask records were written by this same wave with vector stores: drain them to L2
-    // before the scalar loads of the dgrad epilogues read them back
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
     // ---- dgrad chain, l = n-1 .. 1 : dfeat_l = W_l^T dz_{l+1}; dz_l = dfeat_l * relu'(feat_l)
@@ -226,9 +223,10 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     for (int l = nl - 1; l >= 1; --l) {
         const int R = net.Kp[l], Kk = net.Mt[l], n_rt = R / 32;
         f32x16 acc[RT][PT];
+        const uint4 mw = *mask_record(a.mask_bits[l], blockIdx.x, wave, lane);  // in flight behind the GEMM
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
         __syncthreads();
-        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l], slot0);
+        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, mw);
         __syncthreads();
         if (l <= 4) STAMP(15 - l);  // 14 .. 11
         save_tile<P>(st, act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, net.Mt[l - 1] / P::KS);
