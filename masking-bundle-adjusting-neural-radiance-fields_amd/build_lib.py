@@ -30,7 +30,8 @@ def _stale():
 
 def build(force=False, verbose=True, stamps=False):
     if stamps:
-        return _compile(LIB_STAMPS, ["-DMARF_STAMPS"], verbose)
+        extra = os.environ.get("MARF_EXTRA_FLAGS", "").split()
+        return _compile(LIB_STAMPS, ["-DMARF_STAMPS"] + extra, verbose)
     if not force and not _stale():
         return LIB
     return _compile(LIB, [], verbose)

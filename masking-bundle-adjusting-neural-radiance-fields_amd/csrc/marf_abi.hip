@@ -510,8 +510,8 @@ static void plan_step(const marf_net* n, long long S, StepPlan& p) {
         mxo = std::max(mxo, (long long)n->Mp[l] * n->Kp[l]);
         mxm = std::max(mxm, (long long)n->Mp[l]);
     }
-    p.part = off;
-    off += rup((long long)p.n_chunks * mxo * 4, 256);
+    p.part = off;  // also the fold scratch of the last-layer reduction: 256 groups x (3 Kp + 3)
+    off += rup(std::max((long long)p.n_chunks * mxo, 256LL * (3 * n->Kp[nl - 1] + 3)) * 4, 256);
     p.bpart = off;
     off += rup((long long)p.n_chunks * mxm * 4, 256);
     p.total = off;
@@ -605,7 +605,7 @@ int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void
         MarfProfScope ps("wgrad_last_reduce", s);
         HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.wlast), (const float*)(sv + p.blast), p.n_tiles, 3,
                                         net->Kp[l], 3, net->dims[l], d_dparams + net->w_off[l],
-                                        d_dparams + net->b_off[l], s, d_gout, denom),
+                                        d_dparams + net->b_off[l], s, d_gout, denom, part),
                "step_backward last reduce");
     }
     if (d_dh) {

@@ -84,7 +84,7 @@ hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* fea
                                   int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s);
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
                                     int Ko, float* dW, float* db, hipStream_t s, const float* gscale = nullptr,
-                                    const float* denom = nullptr);
+                                    const float* denom = nullptr, float* scratch = nullptr);
 hipError_t marf_launch_mlp_step(const marf::StepArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
 hipError_t marf_launch_loss_final(const double* part, int n, float* out, const float* denom_override, hipStream_t s);
 hipError_t marf_launch_mse(const float* pred, const float* gt, const float* mask, int B, int Np, double* part,

@@ -74,11 +74,20 @@ struct TileStore {
     }
     MARF_DEV void one(const T* src) {
         constexpr int VEC = 16 / sizeof(T);
+#ifdef MARF_DIAG_NO_SAVE
+        q = nq;  // diagnostic: drop the activation stores
+#endif
         if (q < nq) {
             const int r = (q * 4 + wave) * rpi + lr;
             if (r < rows) {
                 const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)r * lda + VEC * lc);
+#ifdef MARF_DIAG_NT
+                typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+                const u32x4_t w = {v.x, v.y, v.z, v.w};
+                __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(dst + (size_t)r * ldd + VEC * lc));
+#else
                 *reinterpret_cast<uint4*>(dst + (size_t)r * ldd + VEC * lc) = v;
+#endif
             }
             ++q;
         }

@@ -299,6 +299,31 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
     }
 }
 
+// First stage of a reduction over many partials (the fused step writes one per pixel tile): group
+// g sums chunks [g*per, (g+1)*per) of partial [n][E] (and bpartial [n][Eb]) into out [G][E]
+// (bout [G][Eb]), in chunk order.  Coalesced over the element index.
+__global__ __launch_bounds__(256) void k_fold_partials(const float* __restrict__ partial, const float* __restrict__ bpartial,
+                                                       int n, int per, long long E, int Eb, float* __restrict__ out,
+                                                       float* __restrict__ bout) {
+    const long long e = blockIdx.x * 256LL + threadIdx.x;
+    const int g = blockIdx.y;
+    const int c0 = g * per, c1 = min(n, c0 + per);
+    if (e < E) {
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        int c = c0;
+        for (; c + 4 <= c1; c += 4)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] += partial[(size_t)(c + u) * E + e];
+        for (int u = 0; c < c1; ++c, ++u) acc[u] += partial[(size_t)c * E + e];
+        out[(size_t)g * E + e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    } else if (e < E + Eb) {
+        const int eb = (int)(e - E);
+        float s = 0.f;
+        for (int c = c0; c < c1; ++c) s += bpartial[(size_t)c * Eb + eb];
+        bout[(size_t)g * Eb + eb] = s;
+    }
+}
+
 }  // namespace marf
 
 using namespace marf;
@@ -368,7 +393,22 @@ hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* fea
 
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
                                     int Ko, float* dW, float* db, hipStream_t s, const float* gscale,
-                                    const float* denom) {
+                                    const float* denom, float* scratch) {
+    if (n_chunks > 1024 && scratch) {
+        // fold into G <= 256 groups first (n_chunks up to millions of partials)
+        const int per = (n_chunks + 255) / 256;
+        const int G = (n_chunks + per - 1) / per;
+        const long long E = (long long)M * K;
+        float* out = scratch;
+        float* bout = scratch + (size_t)G * E;
+        dim3 grid((unsigned)((E + M + 255) / 256), G);
+        hipLaunchKernelGGL(k_fold_partials, grid, dim3(256), 0, s, partial, bpartial, n_chunks, per, E, M, out, bout);
+        hipError_t err = hipGetLastError();
+        if (err != hipSuccess) return err;
+        partial = out;
+        bpartial = bout;
+        n_chunks = G;
+    }
     long long n = (long long)Mo * Ko + Mo;
     int blocks = (int)((n + 63) / 64);
     hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, s, partial, bpartial, n_chunks, M, K, Mo, Ko, dW, db,
