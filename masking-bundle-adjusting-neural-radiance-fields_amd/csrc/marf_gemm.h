@@ -293,34 +293,76 @@ MARF_DEV void c2f_weights_lds(const C2fDev& c2f, int L, float* wsh) {
 
 // Prologue: pixel grid -> sl(3) warp -> posenc (+c2f) of the tile's TP slots -> act [TP][Kp0]
 // (warp.py:33-81, model/planar.py:451-471; feature layout [u, v, sin_k(u), cos_k(u), sin_k(v),
-// cos_k(v)], zero padded to Kp0).  256 / TP threads share a pixel, bands dealt round-robin.
+// cos_k(v)], zero padded to Kp0).  NPART = 256 / TP threads share a pixel: half of them take u,
+// half v, each a contiguous run of bands, written as bf16 pairs (one 4-byte LDS store per pair).
 template <class P, int TP>
 MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh,
                             typename P::T* act, int lda, int b, int p0) {
-    constexpr int NPART = 256 / TP;
+    typedef typename P::T T;
+    constexpr int NPART = 256 / TP, HALF = NPART / 2;
     const int L = net.L;
     const int i = threadIdx.x % TP, part = threadIdx.x / TP;
     float x, y, u = 0.f, v = 0.f, X[3];
     slot_point(geo, b, p0 + i, x, y, u, v, X);
-    typename P::T* row = act + (size_t)i * lda;
-    if (part == NPART - 1) {
-        row[0] = P::cvt(u);
-        row[1] = P::cvt(v);
-    }
-    // band q = c*L + k of coordinate c: sin at 2 + 2cL + k, cos at 2 + 2cL + L + k
-    for (int q = part; q < 2 * L; q += NPART) {
-        const int c = q >= L, k = q - c * L;
-        float s, co;
-        band_sincos<sizeof(typename P::T) == 2>(c ? v : u, k, s, co);
-        if (c2f_on) {
-            const float w = wsh[k];
-            s = s * w;
-            co = co * w;
+    T* row = act + (size_t)i * lda;
+    auto put2 = [&](int col, float a0, float a1) {  // col even
+        if constexpr (sizeof(T) == 2) {
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<uint32_t*>(row + col) =
+                __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){a0, a1}), bf16x2));
+        } else {
+            row[col] = a0;
+            row[col + 1] = a1;
         }
-        row[2 + q + c * L] = P::cvt(s);
-        row[2 + q + c * L + L] = P::cvt(co);
+    };
+    if (part == NPART - 1) put2(0, u, v);
+    if (L > 0) {
+        const int c = part / HALF, sub = part - c * HALF;
+        const float cv = c ? v : u;
+        const int k0 = sub * L / HALF, k1 = (sub + 1) * L / HALF;
+        const int cs = 2 + 2 * c * L, cc = cs + L;  // first sin / cos column of coordinate c
+        int k = k0;
+        auto band = [&](int kk, float& sv, float& cvv) {
+            band_sincos<sizeof(T) == 2>(cv, kk, sv, cvv);
+            if (c2f_on) {
+                const float w = wsh[kk];
+                sv = sv * w;
+                cvv = cvv * w;
+            }
+        };
+        if ((k & 1) && k < k1) {  // odd start: single band
+            float s0, c0;
+            band(k, s0, c0);
+            row[cs + k] = P::cvt(s0);
+            row[cc + k] = P::cvt(c0);
+            ++k;
+        }
+        for (; k + 1 < k1; k += 2) {
+            float s0, c0, s1, c1;
+            band(k, s0, c0);
+            band(k + 1, s1, c1);
+            if ((cs & 1) == 0) {
+                put2(cs + k, s0, s1);
+            } else {
+                row[cs + k] = P::cvt(s0);
+                row[cs + k + 1] = P::cvt(s1);
+            }
+            if (((cc + k) & 1) == 0) {
+                put2(cc + k, c0, c1);
+            } else {
+                row[cc + k] = P::cvt(c0);
+                row[cc + k + 1] = P::cvt(c1);
+            }
+        }
+        if (k < k1) {
+            float s0, c0;
+            band(k, s0, c0);
+            row[cs + k] = P::cvt(s0);
+            row[cc + k] = P::cvt(c0);
+        }
     }
-    for (int f = net.D + part; f < net.Kp[0]; f += NPART) row[f] = P::cvt(0.f);
+    for (int f = net.D + 2 * part; f < net.Kp[0]; f += 2 * NPART) put2(f, 0.f, 0.f);  // D, Kp0 even
 }
 
 // ReLU mask records: one uint4 per lane per (tile, layer) at ((tile * 4 + wave) * 64 + lane), i.e.

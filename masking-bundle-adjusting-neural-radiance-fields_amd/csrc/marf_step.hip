@@ -64,9 +64,19 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     const int Np = a.geo.Np;
 
     STAMP(0);
+    // target + mask of the tile's slots: loaded now, parked in gl until the loss needs them
+    float4 tg = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((int)threadIdx.x < TP && p0 + (int)threadIdx.x < Np) {
+        const int p = p0 + threadIdx.x;
+        tg.x = a.gt[((size_t)b * 3 + 0) * Np + p];
+        tg.y = a.gt[((size_t)b * 3 + 1) * Np + p];
+        tg.z = a.gt[((size_t)b * 3 + 2) * Np + p];
+        tg.w = a.mask ? a.mask[(size_t)b * Np + p] : 1.0f;
+    }
     c2f_weights_lds(a.c2f, net.L, wsh);
     __syncthreads();
     tile_prologue<P, TP>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0);
+    if ((int)threadIdx.x < TP) *reinterpret_cast<float4*>(&gl[threadIdx.x][0]) = tg;
     __syncthreads();
     STAMP(1);
     // every saved tile streams out during the GEMM that reads it next (TileStore)
@@ -115,8 +125,10 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
                 const int p = p0 + px;
                 float g[3] = {0.f, 0.f, 0.f};
                 float sq = 0.f, mv = 0.f;
+                const float4 tv = *reinterpret_cast<const float4*>(&gl[px][0]);  // prefetched target, mask
+                const float tgt[3] = {tv.x, tv.y, tv.z};
                 if (p < Np) {
-                    const float m = a.mask ? a.mask[(size_t)b * Np + p] : 1.0f;
+                    const float m = tv.w;
                     float* o = a.rgb ? a.rgb + ((size_t)b * Np + p) * 3 : nullptr;
 #pragma unroll
                     for (int c = 0; c < 3; ++c) {
@@ -124,7 +136,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
                         const float y = 1.0f / (1.0f + expf(-z));
                         if (o) o[c] = y;
                         // model/planar.py:388-390 and its autograd: x = (p - g) m, d = 2 x m
-                        const float x = (y - a.gt[((size_t)b * 3 + c) * Np + p]) * m;
+                        const float x = (y - tgt[c]) * m;
                         sq += x * x;
                         const float d = (2.0f * x) * m;
                         g[c] = (d * (1.0f - y)) * y;  // torch sigmoid_backward
