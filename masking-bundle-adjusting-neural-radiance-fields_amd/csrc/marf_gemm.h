@@ -38,25 +38,27 @@ MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int col
     }
 }
 
-// Streams an LDS tile [rows][lda] (first `cols` columns) to global [rows][ldd] in 16-byte chunks,
-// `per` chunks per issue() call.  gemm_rows calls issue() once per k-step, so a layer's saved
-// activations leave while the next GEMM (which reads the same tile) runs: stores issued as one
-// burst in front of the GEMM would sit ahead of its weight loads in the in-order vmcnt queue and
-// stall the first MFMA until the whole burst has drained.  bf16 tiles only (16-B aligned rows).
+// Streams an LDS tile [rows][lda] (first `cols` columns) to global [rows][ldd] in 16-byte chunks
+// while the next GEMM (which reads the same tile) runs: one chunk per lane per k-step, issued
+// branch-free (row and step index clamped, so surplus steps rewrite the last chunk with the same
+// bytes) so the compiler's vmcnt / lgkmcnt bookkeeping stays exact and the weight loads of the
+// ring are never waited for behind a store they do not depend on.  Chunks left over when the
+// GEMM has fewer k-steps than the job flush after it.  bf16 tiles only (16-B aligned LDS rows).
+//
+// Wave-uniform walk: rpi = 64 / nch whole rows per wave step (lane -> row lane / nch, chunk
+// lane % nch); wave w copies row groups w, w + 4, ...
 template <class T>
 struct TileStore {
-    // Wave-uniform walk: one issue = one 16-B chunk per lane covering rpi = 64 / nch whole rows
-    // (lane -> row lane / nch, chunk lane % nch); wave w copies row groups w, w + 4, ...  The
-    // source is the LDS tile the GEMM reads (passed to issue()); an idle job has q == nq.
     T* dst;
-    int lda, ldd, rows, rpi, q, nq, per, wave;
+    int lda, ldd, rows, rpi, q, nq, wave;
     int lr, lc;  // per lane
+    bool active;
 
     MARF_DEV void clear() {
+        active = false;
         q = nq = 0;
-        per = 0;
     }
-    MARF_DEV void init(int lda_, T* d, int ldd_, int rows_, int cols, int nk, int wave_, int lane) {
+    MARF_DEV void init(int lda_, T* d, int ldd_, int rows_, int cols, int wave_, int lane) {
         constexpr int VEC = 16 / sizeof(T);
         const int nch = cols / VEC;  // <= 64 (cols <= 512)
         dst = d;
@@ -67,36 +69,28 @@ struct TileStore {
         rpi = 64 / nch;
         lr = lane / nch;
         lc = lane - lr * nch;
-        if (lr >= rpi) lr = 1 << 20;  // idle lane (64 % nch)
         q = 0;
         nq = (rows + 4 * rpi - 1) / (4 * rpi);
-        per = (nq + nk - 1) / nk;
+        active = true;
     }
-    MARF_DEV void one(const T* src) {
+    MARF_DEV int row() const {
+        const int qq = q < nq ? q : nq - 1;
+        const int r = (qq * 4 + wave) * rpi + lr;
+        return r < rows ? r : rows - 1;  // idle lanes / surplus rows repeat the last row's chunk
+    }
+    MARF_DEV uint4 read(const T* src) const {
         constexpr int VEC = 16 / sizeof(T);
-#ifdef MARF_DIAG_NO_SAVE
-        q = nq;  // diagnostic: drop the activation stores
-#endif
-        if (q < nq) {
-            const int r = (q * 4 + wave) * rpi + lr;
-            if (r < rows) {
-                const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)r * lda + VEC * lc);
-#ifdef MARF_DIAG_NT
-                typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-                const u32x4_t w = {v.x, v.y, v.z, v.w};
-                __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(dst + (size_t)r * ldd + VEC * lc));
-#else
-                *reinterpret_cast<uint4*>(dst + (size_t)r * ldd + VEC * lc) = v;
-#endif
-            }
-            ++q;
-        }
+        return *reinterpret_cast<const uint4*>(src + (size_t)row() * lda + VEC * lc);
     }
-    MARF_DEV void issue(const T* src) {
-        for (int u = 0; u < per; ++u) one(src);
+    MARF_DEV void write(uint4 v) {
+        constexpr int VEC = 16 / sizeof(T);
+#ifndef MARF_DIAG_NO_SAVE
+        *reinterpret_cast<uint4*>(dst + (size_t)row() * ldd + VEC * lc) = v;
+#endif
+        ++q;
     }
     MARF_DEV void flush(const T* src) {
-        while (q < nq) one(src);
+        while (q < nq) write(read(src));
     }
 };
 
@@ -107,7 +101,8 @@ struct TileStore {
 // reloaded for k-step k+4 right after its MFMAs issue: three k-steps of latency cover, no register
 // moves), the activation fragments of step k+1 are read from LDS while step k's MFMAs run (two
 // statically named buffers).  Loads past the last k-step are clamped to it (harmless L2 hits).
-template <class P, int NA, int RT, int PT>
+// JOB: one TileStore chunk per k-step (read before the B prefetch, stored after the A reload).
+template <class P, int NA, int RT, int PT, bool JOB>
 MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__ W, int K,
                         const typename P::T* act, int lda, int wave, int lane, TileStore<typename P::T>& st) {
     typedef typename P::frag F;
@@ -135,6 +130,13 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
 #pragma unroll
             for (int i = 0; i < NA; ++i) acc[i][j] = P::mma32(a[i], b[j], acc[i][j]);
     };
+    uint4 sv = make_uint4(0, 0, 0, 0);
+    auto sread = [&]() {
+        if constexpr (JOB) sv = st.read(act);
+    };
+    auto swrite = [&]() {
+        if constexpr (JOB) st.write(sv);
+    };
     F A0[NA], A1[NA], A2[NA], A3[NA], B0[PT], B1[PT];
     if constexpr (sizeof(F) * NA > 32) {
         // wide row blocks (bf16, NA > 2): a 2-deep ring keeps the kernel inside 256 VGPRs
@@ -143,21 +145,23 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
         ldB(B0, 0);
         int k = 0;
         for (; k + 2 <= nk; k += 2) {
+            sread();
             ldB(B1, k + 1);
             __builtin_amdgcn_sched_barrier(0);
             mma(A0, B0);
             __builtin_amdgcn_sched_barrier(0);
             ldA(A0, k + 2);
+            swrite();
+            sread();
             ldB(B0, k + 2);
-            st.issue(act);
             __builtin_amdgcn_sched_barrier(0);
             mma(A1, B1);
             __builtin_amdgcn_sched_barrier(0);
             ldA(A1, k + 3);
-            st.issue(act);
+            swrite();
         }
         if (k < nk) mma(A0, B0);
-        st.flush(act);
+        if constexpr (JOB) st.flush(act);
         return;
     }
     ldA(A0, 0);
@@ -169,30 +173,34 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
     // sched_barrier pins the issue order: left alone, the scheduler sinks every weight load to
     // the loop end (one MFMA of latency cover) and folds the two B buffers into one.
     for (; k + 4 <= nk; k += 4) {
+        sread();
         ldB(B1, k + 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(A0, B0);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A0, k + 4);
+        swrite();
+        sread();
         ldB(B0, k + 2);
-        st.issue(act);
         __builtin_amdgcn_sched_barrier(0);
         mma(A1, B1);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A1, k + 5);
+        swrite();
+        sread();
         ldB(B1, k + 3);
-        st.issue(act);
         __builtin_amdgcn_sched_barrier(0);
         mma(A2, B0);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A2, k + 6);
+        swrite();
+        sread();
         ldB(B0, k + 4);
-        st.issue(act);
         __builtin_amdgcn_sched_barrier(0);
         mma(A3, B1);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A3, k + 7);
-        st.issue(act);
+        swrite();
     }
     // remainder (nk % 4 steps): A0..A2 hold steps k..k+2, B0 holds step k
     if (k < nk) {
@@ -204,7 +212,7 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
             if (k + 2 < nk) mma(A2, B0);
         }
     }
-    st.flush(act);
+    if constexpr (JOB) st.flush(act);
 }
 
 // Accumulators start at the bias of their output row when `bias` is given (so the epilogue does
@@ -233,12 +241,22 @@ MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
     }
     int na = (n_rt - wave + 3) / 4;
     na = na < 0 ? 0 : (na > RT ? RT : na);
-    switch (na) {
-        case 1: gemm_rows<P, 1, RT, PT>(acc, W, K, act, lda, wave, lane, st); break;
-        case 2: gemm_rows<P, 2, RT, PT>(acc, W, K, act, lda, wave, lane, st); break;
-        case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT>(acc, W, K, act, lda, wave, lane, st); break;
-        case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT>(acc, W, K, act, lda, wave, lane, st); break;
-        default: st.flush(act); break;
+    if (st.active) {
+        switch (na) {
+            case 1: gemm_rows<P, 1, RT, PT, true>(acc, W, K, act, lda, wave, lane, st); break;
+            case 2: gemm_rows<P, 2, RT, PT, true>(acc, W, K, act, lda, wave, lane, st); break;
+            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, true>(acc, W, K, act, lda, wave, lane, st); break;
+            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, true>(acc, W, K, act, lda, wave, lane, st); break;
+            default: st.flush(act); break;
+        }
+    } else {
+        switch (na) {
+            case 1: gemm_rows<P, 1, RT, PT, false>(acc, W, K, act, lda, wave, lane, st); break;
+            case 2: gemm_rows<P, 2, RT, PT, false>(acc, W, K, act, lda, wave, lane, st); break;
+            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, false>(acc, W, K, act, lda, wave, lane, st); break;
+            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, false>(acc, W, K, act, lda, wave, lane, st); break;
+            default: break;
+        }
     }
 }
 
@@ -276,7 +294,7 @@ MARF_DEV void save_tile(TileStore<typename P::T>& job, const typename P::T* act,
                         typename P::T* dst, int nk_next) {
     if constexpr (sizeof(typename P::T) == 2) {
         const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        job.init(lda, dst, cols, rows, cols, nk_next > 0 ? nk_next : 1, wave, lane);
+        job.init(lda, dst, cols, rows, cols, wave, lane);
     } else {
         copy_tile_out<P>(act, lda, rows, cols, dst, cols);
         job.clear();

@@ -40,6 +40,14 @@ MARF_DEV i16x4 tr_read16(const u16* p) {
 #define STAMP(i) do { } while (0)
 #endif
 
+// Diagnostic (MARF_DIAG_STORE_L2): every block writes its saved tiles into one of 64 small regions
+// at the start of dz_1 (<= 64 * TP * 512 elements, L2-resident) instead of its own rows.
+#ifdef MARF_DIAG_STORE_L2
+#define SAVE_DST(ptr, cols) (reinterpret_cast<T*>(a.dz[1]) + (size_t)(blockIdx.x & 63) * TP * (cols))
+#else
+#define SAVE_DST(ptr, cols) (ptr)
+#endif
+
 template <class P, int TP>
 __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     typedef typename P::T T;
@@ -81,7 +89,8 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     STAMP(1);
     // every saved tile streams out during the GEMM that reads it next (TileStore)
     TileStore<T> st;
-    save_tile<P>(st, act, lda, TP, net.Kp[0], reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0] / P::KS);
+    save_tile<P>(st, act, lda, TP, net.Kp[0], SAVE_DST(reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0]),
+                 net.Kp[0] / P::KS);
 
     // ---- hidden layers (forward)
     for (int l = 0; l < nl - 1; ++l) {
@@ -95,7 +104,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         if (l < 3) STAMP(3 + 2 * l);
         st.clear();
         if (l + 1 < nl - 1)  // the last layer's input never leaves LDS
-            save_tile<P>(st, act, lda, TP, M, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M / P::KS);
+            save_tile<P>(st, act, lda, TP, M, SAVE_DST(reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M), M / P::KS);
     }
 
     // ---- last layer (3 outputs, rows padded to 16): 16x16 MFMA, TP/4 pixels per wave, sigmoid,
@@ -241,7 +250,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, mw);
         __syncthreads();
         if (l <= 4) STAMP(15 - l);  // 14 .. 11
-        save_tile<P>(st, act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, net.Mt[l - 1] / P::KS);
+        save_tile<P>(st, act, lda, TP, R, SAVE_DST(reinterpret_cast<T*>(a.dz[l]) + slot0 * R, R), net.Mt[l - 1] / P::KS);
     }
 
     // ---- layer-0 dgrad + posenc / warp adjoint -> dH partial
