@@ -39,18 +39,18 @@ MARF_DEV i16x4 tr_read(const u16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
 }
 
-template <class P, int RT, int CT>
+template <class P, int RT, int CT, int SP>
 __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
     typedef typename P::T T;
     constexpr int BM = WgGeo<RT, CT>::BM, BN = WgGeo<RT, CT>::BN;
     constexpr int PADE = sizeof(T) == 2 ? 32 : 4;  // row padding (elements), keeps rows 16-B aligned
     constexpr int LDZ = BM + PADE, LDF = BN + PADE;
     constexpr int VEC = 16 / sizeof(T);          // elements per 16-byte vector
-    constexpr int NVZ = 64 * BM / VEC / 512;     // dz vectors per thread and stage
-    constexpr int NVF = 64 * BN / VEC / 512;     // feat vectors per thread and stage
+    constexpr int NVZ = SP * BM / VEC / 512;     // dz vectors per thread and stage
+    constexpr int NVF = SP * BN / VEC / 512;     // feat vectors per thread and stage
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    T* tz = reinterpret_cast<T*>(smem);          // [64][LDZ]
-    T* tf = tz + 64 * LDZ;                        // [64][LDF]
+    T* tz = reinterpret_cast<T*>(smem);          // [SP][LDZ]
+    T* tf = tz + SP * LDZ;                        // [SP][LDF]
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wr = wave >> 1, wc = wave & 1;
     const int chunk_id = blockIdx.x;
@@ -103,24 +103,24 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
     };
 
     if (s_begin < s_end) load_stage(s_begin);
-    for (long long s0 = s_begin; s0 < s_end; s0 += 64) {
+    for (long long s0 = s_begin; s0 < s_end; s0 += SP) {
         __syncthreads();  // previous stage fully consumed
         store_stage();
         __syncthreads();
-        if (s0 + 64 < s_end) load_stage(s0 + 64);  // next stage in flight behind the MFMAs
+        if (s0 + SP < s_end) load_stage(s0 + SP);  // next stage in flight behind the MFMAs
 
         if (do_bias) {
             // db partial: thread t sums column t%BM over rows t/BM, t/BM + 512/BM, ...
             constexpr int RSTEP = 512 / BM > 0 ? 512 / BM : 1;
             const int c = threadIdx.x % BM, r0 = threadIdx.x / BM;
             if (r0 < RSTEP)
-                for (int r = r0; r < 64; r += RSTEP) bsum += P::tof(tz[r * LDZ + c]);
+                for (int r = r0; r < SP; r += RSTEP) bsum += P::tof(tz[r * LDZ + c]);
         }
 
         if constexpr (sizeof(T) == 2) {
             const int g = lane >> 4, gi = lane & 15, q = gi >> 2, p4 = gi & 3;
 #pragma unroll
-            for (int ks = 0; ks < 64; ks += 16) {
+            for (int ks = 0; ks < SP; ks += 16) {
                 const int r0 = ks + 8 * (g >> 1) + q;  // this lane supplies row r0 (and r0 + 4)
                 typename P::frag af[RT], bf[CT];
 #pragma unroll
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
             }
         } else {
             const int h = lane >> 5, rl = lane & 31;
-            for (int ks = 0; ks < 64; ks += 2) {
+            for (int ks = 0; ks < SP; ks += 2) {
                 typename P::frag af[RT], bf[CT];
 #pragma unroll
                 for (int i = 0; i < RT; ++i) af[i] = tz[(ks + h) * LDZ + (wr * RT + i) * 32 + rl];
@@ -331,17 +331,18 @@ using namespace marf;
 template <class P, int RT, int CT>
 static hipError_t launch_wg(const WgArgs& a, int n_chunks, int n_oblk, hipStream_t s) {
     typedef typename P::T T;
+    constexpr int SP = 64;  // pixels per stage (128 measured slower: register pressure / spills)
     constexpr int BM = WgGeo<RT, CT>::BM, BN = WgGeo<RT, CT>::BN;
     constexpr int PADE = sizeof(T) == 2 ? 32 : 4;
-    size_t lds = (size_t)64 * (BM + PADE + BN + PADE) * sizeof(T);
+    size_t lds = (size_t)SP * (BM + PADE + BN + PADE) * sizeof(T);
     if (lds < 512 * sizeof(float)) lds = 512 * sizeof(float);
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_wgrad<P, RT, CT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipError_t e = hipFuncSetAttribute((const void*)k_wgrad<P, RT, CT, SP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_wgrad<P, RT, CT>), dim3(n_chunks, n_oblk), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((k_wgrad<P, RT, CT, SP>), dim3(n_chunks, n_oblk), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 
