@@ -137,7 +137,7 @@ int marf_profile_enable(int on);
 int marf_profile_reset(void);
 int marf_profile_read(char* names, int name_len, double* total_ms, long long* count, int cap);
 
-/* ---- Diagnostics: device buffer [n_tiles][16] (u64) receiving the fused step's per-phase
+/* ---- Diagnostics: device buffer [n_tiles][32] (u64) receiving the fused step's per-phase
  * s_memtime stamps; only a library built with -DMARF_STAMPS writes it (tools/phase_stamps.py). */
 void marf_debug_set_stamps(void* d_stamps);
 

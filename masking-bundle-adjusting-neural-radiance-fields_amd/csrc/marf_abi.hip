@@ -58,7 +58,7 @@ extern "C" {
 
 const char* marf_last_error(void) { return g_err.c_str(); }
 
-// Diagnostic builds only: device buffer [n_tiles][16] for the fused step's phase stamps.
+// Diagnostic builds only: device buffer [n_tiles][32] for the fused step's phase stamps.
 void marf_debug_set_stamps(void* d_stamps) { g_stamps = (unsigned long long*)d_stamps; }
 int marf_version(void) { return 1; }
 
@@ -474,7 +474,7 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
 
 struct StepPlan {
     size_t feat[MARF_MAX_LAYERS], dz[MARF_MAX_LAYERS], mask[MARF_MAX_LAYERS];
-    size_t wlast, blast, dH, loss, part, bpart, total;
+    size_t wlast, blast, dH, loss, c2f, part, bpart, total;
     int n_tiles, chunk, n_chunks;
 };
 
@@ -501,6 +501,8 @@ static void plan_step(const marf_net* n, long long S, StepPlan& p) {
     off += rup((long long)p.n_tiles * 9 * 4, 256);
     p.loss = off;
     off += rup((long long)p.n_tiles * 2 * 8, 256);
+    p.c2f = off;
+    off += 256;
     long long chunk = rup((S + 255) / 256, 64);
     if (chunk < 64) chunk = 64;
     p.chunk = (int)chunk;
@@ -555,7 +557,9 @@ int marf_step_forward(const marf_net* net, const marf_geometry* geo, const marf_
     a.blast_partial = (float*)(sv + p.blast);
     a.dH_partial = (float*)(sv + p.dH);
     a.loss_partial = (double*)(sv + p.loss);
+    a.c2f_w = (const float*)(sv + p.c2f);
     a.stamps = g_stamps;
+    if (net->L > 0) HIPCHK(marf_launch_c2f_weights(a.c2f, net->L, (float*)(sv + p.c2f), s), "step_forward c2f");
     {
         MarfProfScope ps("mlp_step", s);
         HIPCHK(marf_launch_mlp_step(a, net->dtype, net->TP, net->lds_step, p.n_tiles, s), "step_forward");

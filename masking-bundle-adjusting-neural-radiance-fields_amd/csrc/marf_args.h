@@ -52,7 +52,8 @@ struct StepArgs {
     float* blast_partial;                   // out: [n_tiles][3]
     float* dH_partial;                      // out: [n_tiles][9]
     double* loss_partial;                   // out: [n_tiles][2] = sum ((p - g) m)^2, sum m
-    unsigned long long* stamps;             // diagnostic builds (MARF_STAMPS): [n_tiles][16] s_memtime
+    const float* c2f_w;                     // [L] band weights of this step (k_c2f_weights)
+    unsigned long long* stamps;             // diagnostic builds (MARF_STAMPS): [n_tiles][32] s_memtime
     long long S;
     int lda;
 };
@@ -86,6 +87,7 @@ hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial,
                                     int Ko, float* dW, float* db, hipStream_t s, const float* gscale = nullptr,
                                     const float* denom = nullptr, float* scratch = nullptr);
 hipError_t marf_launch_mlp_step(const marf::StepArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
+hipError_t marf_launch_c2f_weights(const marf::C2fDev& c, int L, float* out, hipStream_t s);
 hipError_t marf_launch_loss_final(const double* part, int n, float* out, const float* denom_override, hipStream_t s);
 hipError_t marf_launch_mse(const float* pred, const float* gt, const float* mask, int B, int Np, double* part,
                            float* out, const float* denom_override, hipStream_t s);

@@ -32,6 +32,19 @@ typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
 #define MARF_DEV __device__ __forceinline__
 
+// Phase timestamps (diagnostic builds only, -DMARF_STAMPS; tools/phase_stamps.py): wave 0 of a
+// block writes s_memtime into slot i of its row sp (32 slots per block).
+#ifdef MARF_STAMPS
+#define MARF_STAMP(sp, i)                                                           \
+    do {                                                                            \
+        if ((sp) && threadIdx.x == 0) (sp)[i] = __builtin_amdgcn_s_memtime();       \
+    } while (0)
+#else
+#define MARF_STAMP(sp, i) \
+    do {                  \
+    } while (0)
+#endif
+
 // ------------------------------------------------------------------ bf16 helpers
 
 MARF_DEV u16 f2bf(float x) {
@@ -214,8 +227,38 @@ MARF_DEV void band_sincos(float c, int k, float& s, float& co) {
     }
 }
 
-MARF_DEV float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Wave reductions on the DPP network (no LDS traffic): quad swaps, row rotations, then the gfx9
+// row broadcasts; fixed order, the total lands in lane 63.
+template <int CTRL, int ROWMASK = 0xf>
+MARF_DEV int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWMASK, 0xf, false);
+}
+template <int CTRL, int ROWMASK = 0xf>
+MARF_DEV float dpp_f(float v) {
+    return __int_as_float(dpp_i<CTRL, ROWMASK>(__float_as_int(v)));
+}
+template <int CTRL, int ROWMASK = 0xf>
+MARF_DEV double dpp_d(double v) {
+    const long long u = __double_as_longlong(v);
+    const int lo = dpp_i<CTRL, ROWMASK>((int)(u & 0xffffffffLL)), hi = dpp_i<CTRL, ROWMASK>((int)(u >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <class V>
+MARF_DEV V wave_total63(V v) {
+    if constexpr (sizeof(V) == 8) {
+        v += dpp_d<0xB1>(v);        // quad_perm [1,0,3,2]
+        v += dpp_d<0x4E>(v);        // quad_perm [2,3,0,1]
+        v += dpp_d<0x124>(v);       // row_ror:4
+        v += dpp_d<0x128>(v);       // row_ror:8   -> every lane holds its row's sum
+        v += dpp_d<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+        v += dpp_d<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+    } else {
+        v += dpp_f<0xB1>(v);
+        v += dpp_f<0x4E>(v);
+        v += dpp_f<0x124>(v);
+        v += dpp_f<0x128>(v);
+        v += dpp_f<0x142, 0xa>(v);
+        v += dpp_f<0x143, 0xc>(v);
+    }
     return v;
 }

@@ -467,7 +467,7 @@ MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
 template <class P, int TP>
 MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh, char* smem, int lda,
                            int wave, int lane, int b, int p0, float* red, float* red9, float* dH_partial,
-                           float* d_coords, TileStore<typename P::T>& st) {
+                           float* d_coords, TileStore<typename P::T>& st, unsigned long long* sp = nullptr) {
     typedef typename P::T T;
     constexpr int PT = TP / 32;
     constexpr int RT = 8 / PT;
@@ -477,6 +477,7 @@ MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, con
     f32x16 acc[RT][PT];
     gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[0]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
     __syncthreads();
+    MARF_STAMP(sp, 16);
     float* df = reinterpret_cast<float*>(smem);
     const int ldf = R + 1;
 #pragma unroll
@@ -491,6 +492,7 @@ MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, con
         }
     }
     __syncthreads();
+    MARF_STAMP(sp, 17);
 
     // posenc adjoint: d coord_c = df[c] + sum_k w_k f_k (cos(x_k) df_sin - sin(x_k) df_cos)
     constexpr int NPART = 256 / TP;
@@ -520,6 +522,7 @@ MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, con
     red[(part * TP + i) * 2] = du;
     red[(part * TP + i) * 2 + 1] = dv;
     __syncthreads();
+    MARF_STAMP(sp, 18);
     float h9[9];
 #pragma unroll
     for (int e = 0; e < 9; ++e) h9[e] = 0.f;
@@ -553,8 +556,8 @@ MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, con
     if (geo.mode == 0) {
 #pragma unroll
         for (int e = 0; e < 9; ++e) {
-            float s = wave_sum(h9[e]);
-            if (lane == 0) red9[wave * 9 + e] = s;
+            const float s = wave_total63(h9[e]);
+            if (lane == 63) red9[wave * 9 + e] = s;
         }
         __syncthreads();
         if (threadIdx.x < 9) {

@@ -30,15 +30,7 @@ MARF_DEV i16x4 tr_read16(const u16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
 }
 
-// Phase timestamps of wave 0 (diagnostic build only: -DMARF_STAMPS, tools/phase_stamps.py).
-#ifdef MARF_STAMPS
-#define STAMP(i)                                                                                   \
-    do {                                                                                           \
-        if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#else
-#define STAMP(i) do { } while (0)
-#endif
+#define STAMP(i) MARF_STAMP(sp, i)
 
 // Diagnostic (MARF_DIAG_STORE_L2): every block writes its saved tiles into one of 64 small regions
 // at the start of dz_1 (<= 64 * TP * 512 elements, L2-resident) instead of its own rows.
@@ -70,6 +62,9 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     tile_origin(a.geo, blockIdx.x, TP, b, p0, slot0);
     const int nl = net.n_layers;
     const int Np = a.geo.Np;
+#ifdef MARF_STAMPS
+    unsigned long long* sp = a.stamps ? a.stamps + (size_t)blockIdx.x * 32 : nullptr;
+#endif
 
     STAMP(0);
     // target + mask of the tile's slots: loaded now, parked in gl until the loss needs them
@@ -81,8 +76,9 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         tg.z = a.gt[((size_t)b * 3 + 2) * Np + p];
         tg.w = a.mask ? a.mask[(size_t)b * Np + p] : 1.0f;
     }
-    c2f_weights_lds(a.c2f, net.L, wsh);
+    if ((int)threadIdx.x < net.L) wsh[threadIdx.x] = a.c2f_w[threadIdx.x];
     __syncthreads();
+    STAMP(19);
     tile_prologue<P, TP>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0);
     if ((int)threadIdx.x < TP) *reinterpret_cast<float4*>(&gl[threadIdx.x][0]) = tg;
     __syncthreads();
@@ -92,8 +88,9 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     save_tile<P>(st, act, lda, TP, net.Kp[0], SAVE_DST(reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0]),
                  net.Kp[0] / P::KS);
 
-    // ---- hidden layers (forward)
-    for (int l = 0; l < nl - 1; ++l) {
+    // ---- hidden layers (forward); the last one is peeled so the last layer's weight fragments
+    //      can be in flight behind its epilogue without pinning registers through the loop
+    auto hidden = [&](int l) {
         const int K = net.Kp[l], M = net.Mp[l], n_rt = M / 32;
         f32x16 acc[RT][PT];
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l], st);
@@ -105,6 +102,24 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         st.clear();
         if (l + 1 < nl - 1)  // the last layer's input never leaves LDS
             save_tile<P>(st, act, lda, TP, M, SAVE_DST(reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M), M / P::KS);
+    };
+    for (int l = 0; l < nl - 2; ++l) hidden(l);
+    constexpr int NWL = 8;  // prefetched last-layer k-steps (16x16 fragments)
+    typename P::frag wl[NWL];
+    {
+        const int l = nl - 2;
+        const int K = net.Kp[l], M = net.Mp[l], n_rt = M / 32;
+        f32x16 acc[RT][PT];
+        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l], st);
+        __syncthreads();
+        STAMP(2 + 2 * l);
+        const T* W = reinterpret_cast<const T*>(net.Wf[nl - 1]);
+        const int nk16 = net.Kp[nl - 1] / P::KS16;
+#pragma unroll
+        for (int u = 0; u < NWL; ++u) wl[u] = P::load_frag(W + ((size_t)(u < nk16 ? u : 0) * 64 + lane) * P::FE);
+        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x);
+        __syncthreads();
+        st.clear();
     }
 
     // ---- last layer (3 outputs, rows padded to 16): 16x16 MFMA, TP/4 pixels per wave, sigmoid,
@@ -117,12 +132,24 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[j] = (f32x4){};
         const int ko = P::kofs16(lane);
-        for (int k0 = 0; k0 < Kl; k0 += P::KS16) {
-            typename P::frag wa = P::load_frag(W + ((size_t)(k0 / P::KS16) * 64 + lane) * P::FE);
+        const int nk16 = Kl / P::KS16;
+#pragma unroll
+        for (int u = 0; u < NWL; ++u) {
+            if (u < nk16) {
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int px = wave * (TP / 4) + j * 16 + (lane & 15);
+                    typename P::frag bb = P::load_frag(act + (size_t)px * lda + u * P::KS16 + ko);
+                    acc[j] = P::mma16(wl[u], bb, acc[j]);
+                }
+            }
+        }
+        for (int u = NWL; u < nk16; ++u) {
+            typename P::frag wa = P::load_frag(W + ((size_t)u * 64 + lane) * P::FE);
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int px = wave * (TP / 4) + j * 16 + (lane & 15);
-                typename P::frag bb = P::load_frag(act + (size_t)px * lda + k0 + ko);
+                typename P::frag bb = P::load_frag(act + (size_t)px * lda + u * P::KS16 + ko);
                 acc[j] = P::mma16(wa, bb, acc[j]);
             }
         }
@@ -172,12 +199,9 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
             s0 += (double)lsum[0][px];
             s1 += (double)lsum[1][px];
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            s0 += __shfl_xor(s0, o, 64);
-            s1 += __shfl_xor(s1, o, 64);
-        }
-        if (lane == 0) {
+        s0 = wave_total63(s0);
+        s1 = wave_total63(s1);
+        if (lane == 63) {
             a.loss_partial[2 * (size_t)blockIdx.x] = s0;
             a.loss_partial[2 * (size_t)blockIdx.x + 1] = s1;
         }
@@ -188,8 +212,8 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
             for (int c = 0; c < 3; ++c) s[c] += gl[px][c];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const float t = wave_sum(s[c]);
-            if (lane == c) a.blast_partial[(size_t)blockIdx.x * 3 + c] = t;
+            const float t = wave_total63(s[c]);
+            if (lane == 63) a.blast_partial[(size_t)blockIdx.x * 3 + c] = t;
         }
     }
 
@@ -254,8 +278,17 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     }
 
     // ---- layer-0 dgrad + posenc / warp adjoint -> dH partial
+#ifdef MARF_STAMPS
+    warp_adjoint<P, TP>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st, sp);
+#else
     warp_adjoint<P, TP>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st);
+#endif
     STAMP(15);
+}
+
+// The step's c2f band weights, once (model/planar.py:462-470; 1 without c2f).
+__global__ void k_c2f_weights(C2fDev c, int L, float* __restrict__ out) {
+    if ((int)threadIdx.x < L) out[threadIdx.x] = c.on ? c2f_weight(*c.progress, c.start, c.span, L, threadIdx.x) : 1.0f;
 }
 
 // Loss of the fused step from the per-tile partials (fp64, fixed-order tree):
@@ -306,6 +339,11 @@ static hipError_t launch_step_t(const StepArgs& a, size_t lds, int n_tiles, hipS
 hipError_t marf_launch_mlp_step(const StepArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s) {
     if (dtype == 1) return TP == 128 ? launch_step_t<PrecBF16, 128>(a, lds, n_tiles, s) : launch_step_t<PrecBF16, 64>(a, lds, n_tiles, s);
     return TP == 128 ? launch_step_t<PrecF32, 128>(a, lds, n_tiles, s) : launch_step_t<PrecF32, 64>(a, lds, n_tiles, s);
+}
+
+hipError_t marf_launch_c2f_weights(const C2fDev& c, int L, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_c2f_weights, dim3(1), dim3(64), 0, s, c, L, out);
+    return hipGetLastError();
 }
 
 hipError_t marf_launch_loss_final(const double* part, int n, float* out, const float* denom_override, hipStream_t s) {

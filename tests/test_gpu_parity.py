@@ -484,7 +484,8 @@ def test_bf16_gradients_vs_fp32_c3_width(tmp_path):
     """C3 widths (L=16, 4 x 256 hidden: the LDS-DMA weight-gradient kernel and the 128-pixel
     tiles): bf16 MLP gradients against the fp32 path from the same state (cosine >= 0.995 and
     max error <= 5e-2 of the max per tensor: bf16 features / dz, measured 0.998 / 3.5e-2 on the
-    layer-0 weight; north_star bf16 tolerance class)."""
+    layer-0 weight); warp gradient cosine >= 0.99 against fp32 and <= 2e-2 against the
+    separate-kernel bf16 path."""
     from model import planar
     from util import EasyDict as edict
     B = 2
@@ -493,8 +494,9 @@ def test_bf16_gradients_vs_fp32_c3_width(tmp_path):
     mask = t((rng.random((B, 1, 256, 256)) < 0.85).astype(np.float32))
     warp0 = t((rng.standard_normal((B, 8)) * 0.01).astype(np.float32))
     res = {}
-    for precision in ("fp32", "bf16"):
-        opt = make_opt(tmp_path, H=512, W=512, patch_H=256, patch_W=256, batch_size=B, precision=precision,
+    for precision in ("fp32", "bf16", "bf16-separate"):
+        opt = make_opt(tmp_path, H=512, W=512, patch_H=256, patch_W=256, batch_size=B,
+                       precision=precision.split("-")[0], fused_step=precision != "bf16-separate",
                        arch={"layers": [None, 256, 256, 256, 256, 3], "skip": [], "posenc": {"L_2D": 16}})
         torch.manual_seed(0)
         graph = planar.Graph(opt).to(DEV)
@@ -514,5 +516,16 @@ def test_bf16_gradients_vs_fp32_c3_width(tmp_path):
     print("bf16 vs fp32 (cosine, max rel err):", stats)
     for cos, err in stats:
         assert cos > 0.995 and err <= 5e-2, stats
+    ws = res["bf16-separate"][1]
+    print("warp grad bf16 fused vs separate kernels: max rel err",
+          float((res["bf16"][1] - ws).abs().max() / ws.abs().max()),
+          "separate vs fp32:", float((ws - res["fp32"][1]).abs().max() / res["fp32"][1].abs().max()))
     wa, wb = res["bf16"][1], res["fp32"][1]
-    assert (wa - wb).abs().max() <= 3e-2 * wb.abs().max()
+    werr = float((wa - wb).abs().max() / wb.abs().max())
+    wcos = float((wa * wb).sum() / (wa.norm() * wb.norm()))
+    print("warp grad bf16 vs fp32: cosine", wcos, "max rel err", werr)
+    # bf16 numerics, not the fused kernel: the separate-kernel bf16 path is as far from fp32 (0.11
+    # max rel, cosine 0.994 measured) and within 1e-2 of the fused one; the end-to-end bf16 check
+    # is the trajectory / PSNR test
+    assert wcos > 0.99 and werr <= 0.15, (wcos, werr)
+    assert float((res["bf16"][1] - ws).abs().max() / ws.abs().max()) <= 2e-2

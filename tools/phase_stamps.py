@@ -18,8 +18,11 @@ import marf_hip  # noqa: E402
 from model import planar  # noqa: E402
 from util import EasyDict as edict  # noqa: E402
 
-NAMES = ["prologue", "L0 gemm", "L0 epi", "L1 gemm", "L1 epi", "L2 gemm", "L2 epi", "L3 gemm", "L3 epi+last+loss",
-         "lossred+dWlast", "dg4", "dg3", "dg2", "dg1", "adjoint"]
+# (name, from slot, to slot)
+PHASES = [("start+c2f", 0, 19), ("prologue", 19, 1), ("L0 gemm", 1, 2), ("L0 epi", 2, 3), ("L1 gemm", 3, 4),
+          ("L1 epi", 4, 5), ("L2 gemm", 5, 6), ("L2 epi", 6, 7), ("L3 gemm", 7, 8), ("L3 epi+last+loss", 8, 9),
+          ("lossred+dWlast", 9, 10), ("dg4", 10, 11), ("dg3", 11, 12), ("dg2", 12, 13), ("dg1", 13, 14),
+          ("adj gemm0", 14, 16), ("adj df scatter", 16, 17), ("adj posenc", 17, 18), ("adj warp+dH", 18, 15)]
 
 
 def main():
@@ -37,19 +40,18 @@ def main():
     m.graph.neural_image.progress.data.fill_(0.2)
     var = edict(idx=torch.arange(B), images=m.images)
     n_tiles = B * ((opt.patch_H * opt.patch_W + 127) // 128)
-    st = torch.zeros(n_tiles * 16, dtype=torch.int64, device=dev)
+    st = torch.zeros(n_tiles * 32, dtype=torch.int64, device=dev)
     lib = marf_hip.lib()
     for it in range(3):
         lib.marf_debug_set_stamps(st.data_ptr() if it == 2 else None)
         v = m.graph.forward(var, mode="train")
         torch.cuda.synchronize()
     lib.marf_debug_set_stamps(None)
-    s = st.view(n_tiles, 16).cpu().numpy().astype(np.float64)
-    d = np.diff(s, axis=1)
-    t0 = s[:, 0].min()
-    print(f"tiles {n_tiles}; kernel span {(s[:, 15].max() - t0):.0f} ticks; mean tile life {(s[:, 15] - s[:, 0]).mean():.0f}")
-    for i, nm in enumerate(NAMES):
-        print(f"  {nm:22s} mean {d[:, i].mean():9.0f}  p10 {np.percentile(d[:, i], 10):9.0f}  p90 {np.percentile(d[:, i], 90):9.0f}")
+    s = st.view(n_tiles, 32).cpu().numpy().astype(np.float64)
+    print(f"tiles {n_tiles}; mean tile life {(s[:, 15] - s[:, 0]).mean():.0f} ticks")
+    for nm, a, b in PHASES:
+        d = s[:, b] - s[:, a]
+        print(f"  {nm:22s} mean {d.mean():9.0f}  p10 {np.percentile(d, 10):9.0f}  p90 {np.percentile(d, 90):9.0f}")
 
 
 if __name__ == "__main__":
