@@ -31,7 +31,9 @@ def _stale():
 def build(force=False, verbose=True, stamps=False):
     if stamps:
         extra = os.environ.get("MARF_EXTRA_FLAGS", "").split()
-        return _compile(LIB_STAMPS, ["-DMARF_STAMPS"] + extra, verbose)
+        name = os.environ.get("MARF_LIB_NAME")  # diagnostic variants side by side
+        path = os.path.join(HERE, "lib", name) if name else LIB_STAMPS
+        return _compile(path, ["-DMARF_STAMPS"] + extra, verbose)
     if not force and not _stale():
         return LIB
     return _compile(LIB, [], verbose)

@@ -334,7 +334,11 @@ MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, co
             row[col + 1] = a1;
         }
     };
+#if defined(MARF_DIAG_FEAT_BF16) || defined(MARF_DIAG_FEAT_FP16)
+    if (part == NPART - 1) put2(0, DIAG_RND(u), DIAG_RND(v));
+#else
     if (part == NPART - 1) put2(0, u, v);
+#endif
     if (L > 0) {
         const int c = part / HALF, sub = part - c * HALF;
         const float cv = c ? v : u;
@@ -348,6 +352,10 @@ MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, co
                 sv = sv * w;
                 cvv = cvv * w;
             }
+#if defined(MARF_DIAG_FEAT_BF16) || defined(MARF_DIAG_FEAT_FP16)
+            sv = DIAG_RND(sv);
+            cvv = DIAG_RND(cvv);
+#endif
         };
         if ((k & 1) && k < k1) {  // odd start: single band
             float s0, c0;
@@ -421,6 +429,9 @@ MARF_DEV void relu_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
                     : "v"(acc[i][j][r])
                     : "vcc");
                 o[r] = v;
+#if defined(MARF_DIAG_ACT_BF16) || defined(MARF_DIAG_ACT_FP16)
+                o[r] = DIAG_RND(o[r]);
+#endif
             }
             words[ti >> 1] |= bits << (16 * (1 - (ti & 1)));
 #pragma unroll
@@ -452,6 +463,9 @@ MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
             for (int r = 0; r < 16; ++r) {
                 const int m = __builtin_amdgcn_sbfe((int)w, 16 * (1 - (ti & 1)) + 15 - r, 1);
                 o[r] = __int_as_float(__float_as_int(acc[i][j][r]) & m);
+#ifdef MARF_DIAG_DZ_BF16
+                o[r] = diag_round_bf16(o[r]);
+#endif
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q)

@@ -153,7 +153,13 @@ __global__ void k_pack(const float* __restrict__ params, char* __restrict__ pack
         if (e < nf) {
             int m, k;
             frag_coord<P>(e, nkf, last16, m, k);
-            wf[e] = P::cvt(m < L.M && k < L.K ? W[(size_t)m * L.K + k] : 0.f);
+            float wv = m < L.M && k < L.K ? W[(size_t)m * L.K + k] : 0.f;
+#if defined(MARF_DIAG_W_BF16)
+            wv = diag_round_bf16(wv);
+#elif defined(MARF_DIAG_W_FP16)
+            wv = diag_round_fp16(wv);
+#endif
+            wf[e] = P::cvt(wv);
         } else if (e < nf + nt) {
             int kr, m;  // row of W^T = input feature, column = output feature
             frag_coord<P>(e - nf, nkt, false, kr, m);

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     __shared__ float red[4 * TP * 2];
     __shared__ float red9[4 * 9];
     __shared__ __attribute__((aligned(16))) float gl[TP][4];  // sigmoid' gradient per slot (fp32)
-    __shared__ __attribute__((aligned(16))) T gT[4][TP];      // the same, channel-major, MFMA operand
+    __shared__ __attribute__((aligned(16))) T gT[8][TP];      // the same, channel-major, split hi / lo
     __shared__ float lsum[2][TP];                              // per-slot ((p-g) m)^2 and m
 
     const NetDev& net = a.net;
@@ -180,10 +180,14 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
                     mv = m;
                 }
                 *reinterpret_cast<float4*>(&gl[px][0]) = make_float4(g[0], g[1], g[2], 0.f);
-                gT[0][px] = P::cvt(g[0]);
-                gT[1][px] = P::cvt(g[1]);
-                gT[2][px] = P::cvt(g[2]);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {  // g = hi + lo (bf16 pair: ~16 significant bits)
+                    const T hi = P::cvt(g[c]);
+                    gT[c][px] = hi;
+                    gT[4 + c][px] = P::cvt(g[c] - P::tof(hi));
+                }
                 gT[3][px] = P::cvt(0.f);
+                gT[7][px] = P::cvt(0.f);
                 lsum[0][px] = sq;
                 lsum[1][px] = mv;
             }
@@ -218,8 +222,9 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     }
 
     // ---- last-layer weight gradient of the tile: dW[c][k] = sum_px g[px][c] feat[px][k]
-    //      16x16 MFMA, A = g^T (channels x pixels), B = feat (pixels x features, transposed LDS
-    //      read for bf16); column tiles of 16 features dealt round-robin to the waves.
+    //      16x16 MFMA, A = g^T (rows 0-2: bf16 hi parts of the 3 channels, rows 4-6: lo parts),
+    //      B = feat (pixels x features, transposed LDS read for bf16); hi + lo rows are added
+    //      after the K loop.  Column tiles of 16 features dealt round-robin to the waves.
     {
         float* wout = a.wlast_partial + (size_t)blockIdx.x * 3 * Kl;
         for (int ct = wave; ct < Kl / 16; ct += 4) {
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
 #pragma unroll
                 for (int k0 = 0; k0 < TP; k0 += 32) {
                     bf16x8 fa;
-                    if (gi < 4) fa = *reinterpret_cast<const bf16x8*>(&gT[gi][k0 + 8 * g]);
+                    if (gi < 8) fa = *reinterpret_cast<const bf16x8*>(&gT[gi][k0 + 8 * g]);
                     else fa = (bf16x8){};
                     const int r0 = k0 + 8 * g + (gi >> 2);
                     const u16* base = reinterpret_cast<const u16*>(act) + (size_t)r0 * lda + ct * 16 + 4 * (gi & 3);
@@ -239,15 +244,19 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
             } else {
                 const int kk = lane >> 4, n = lane & 15;
                 for (int k0 = 0; k0 < TP; k0 += 4) {
-                    const float fa = n < 4 ? P::tof(gT[n][k0 + kk]) : 0.f;
+                    const float fa = n < 8 ? P::tof(gT[n][k0 + kk]) : 0.f;
                     const float fb = P::tof(act[(size_t)(k0 + kk) * lda + ct * 16 + n]);
                     acc = P::mma16(fa, fb, acc);
                 }
             }
-            // accumulator: lane l, reg r -> row (channel) 4 (l >> 4) + r, column l & 15
+            // accumulator: lane l, reg r -> row 4 (l >> 4) + r, column l & 15: hi rows in lanes
+            // 0-15, lo rows in lanes 16-31
+            float lo[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) lo[c] = __shfl_down(acc[c], 16, 64);
             if (lane < 16) {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) wout[(size_t)c * Kl + ct * 16 + lane] = acc[c];
+                for (int c = 0; c < 3; ++c) wout[(size_t)c * Kl + ct * 16 + lane] = acc[c] + lo[c];
             }
         }
     }

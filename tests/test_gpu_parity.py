@@ -216,12 +216,12 @@ def test_small_step_bf16(tag, tmp_path):
 
 # ------------------------------------------------------------------------ real C1 (cat_batch3)
 
-def c1_setup(precision, tmp_path):
+def c1_setup(precision, tmp_path, seed=3):
     from model import planar
     from util import EasyDict as edict
     imgs = g("cat_batch3_c1")
     opt = make_opt(tmp_path, precision=precision)
-    torch.manual_seed(3)
+    torch.manual_seed(seed)
     m = planar.Model(opt)
     rgb = t(imgs["rgb"].astype(np.float32) / np.float32(255))
     mask = t(imgs["mask"].astype(np.float32))
@@ -529,3 +529,61 @@ def test_bf16_gradients_vs_fp32_c3_width(tmp_path):
     # is the trajectory / PSNR test
     assert wcos > 0.99 and werr <= 0.15, (wcos, werr)
     assert float((res["bf16"][1] - ws).abs().max() / ws.abs().max()) <= 2e-2
+
+
+# ------------------------------------------------------------------------ end-to-end (3000 steps)
+
+# Reference run (the reference's Graph / Adam imported here through the stub harness,
+# seed 3, cat_batch3, c2f [0, 0.4], L = 8, 3000 iterations): final PSNR and warp rows 1-4.
+REF_PSNR_3000 = 25.9968
+REF_WARPS_3000 = np.array([
+    [0.0261, 0.0157, -0.1039, -0.2977, -0.2514, 0.3742, 0.2342, -0.0366],
+    [0.0395, 0.0649, -0.1035, -0.3085, -0.1911, 0.2518, 0.1570, -0.2290],
+    [0.0108, 0.0645, -0.1077, -0.3024, -0.2708, 0.4147, 0.2506, -0.1590],
+    [0.0209, 0.0826, -0.1087, -0.3075, -0.0772, 0.0255, 0.2322, -0.4001]], dtype=np.float32)
+
+
+def _run_c1(precision, tmp_path, iters=3000, fused=True, seed=3):
+    m, var = c1_setup(precision, tmp_path, seed)
+    m.opt.freq.vis = 10 ** 9
+    m.opt.fused_step = fused
+    psnr = []
+    for s in range(iters):
+        loss = m.train_iteration(var, _Loader())
+        m.graph.warp_param.weight.data[0] = 0  # Model.train's fix_first line
+        if (s + 1) % m.opt.freq.scalar == 0:
+            psnr.append(-10 * np.log10(float(loss.rgb)))
+    return psnr, m.graph.warp_param.weight.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path):
+    """BASELINE config 1/2 end to end: the seed=3 cat_batch3 run for 3000 iterations.
+
+    fp32: final PSNR within 0.05 dB of the reference's 25.9968 dB (north_star) and the recovered
+    warps within 3e-2 of the reference's.  The 6/10-step trajectories match to 1e-5
+    (test_c1_real_init_and_trajectory_fp32); over 3000 Adam steps the different fp32 summation
+    order (MFMA tiles vs the reference's CPU GEMMs) moves every patch by a common ~1-2e-2 offset
+    (measured: max 2.3e-2; our fused vs separate-kernel paths differ by as much).
+
+    bf16: the training outcome on this scene is set by which basin patch 1's perspective row falls
+    into (final PSNR ~22.7 / ~24.9 / ~26.0 dB), for fp32 as well: over 10 network-init seeds fp32
+    reaches 26.0 dB only on seed 3 (tools/seed_sweep.py; profiles/r1_seed_sweep.json, fp32 mean
+    23.92 dB vs bf16 23.66 dB).  Any rounding change (bf16 activations, or even fp16 posenc
+    features alone) re-rolls that basin, so the bf16 assertion is that the run trains into one of
+    the basins fp32 reaches (>= 22.5 dB) -- the 0.05 dB seed-3 bound is an fp32 property."""
+    psnr, warps = _run_c1(precision, tmp_path)
+    print(f"{precision}: final PSNR {psnr[-1]:.4f} dB, mean of last 10 logged {np.mean(psnr[-10:]):.4f} dB; "
+          f"max |warp - ref| {np.abs(warps[1:] - REF_WARPS_3000).max():.2e}")
+    print("warp - ref:\n", np.array2string(warps[1:] - REF_WARPS_3000, precision=4))
+    print("PSNR every 300:", [round(x, 3) for x in psnr[14::15]])
+    if os.environ.get("MARF_C1_SEPARATE"):
+        p2, w2 = _run_c1(precision, tmp_path, fused=False)
+        print(f"{precision} separate kernels: final PSNR {p2[-1]:.4f}; max |warp - fused| {np.abs(w2 - warps).max():.2e}")
+    if precision == "fp32":
+        assert abs(psnr[-1] - REF_PSNR_3000) <= 0.05, psnr[-10:]
+        np.testing.assert_allclose(warps[1:], REF_WARPS_3000, atol=3e-2)
+    else:
+        assert np.mean(psnr[-10:]) >= 22.5, psnr[-10:]
+        assert psnr[-1] > psnr[14] + 2.0, psnr[::15]  # trained well past the 300-step level
+    assert np.all(warps[0] == 0)
