@@ -46,6 +46,35 @@ def flops_per_px(dims):
     return 6 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
 
 
+def step_kernel_bytes(S, Kp0, hidden, elem):
+    """Algorithmic HBM bytes per launch of the store-activations decomposition (each value moved
+    once): the fused step reads targets + masks (16 B/px, fp32) and its own ReLU-mask records back,
+    and writes every saved layer input feat_0..feat_{n-2}, every dz_1..dz_{n-1} (elem bytes per
+    feature), the ReLU-mask records (1 bit per hidden feature) and the per-tile last-layer gradient
+    partials; each weight-gradient kernel reads dz_{l+1} and feat_l once."""
+    n_h = len(hidden)
+    masks = S * sum(hidden) // 8
+    feat = S * elem * (Kp0 + sum(hidden[:-1]))
+    dz = S * elem * sum(hidden)
+    wlast = (S // 128) * 4 * 3 * hidden[-1]
+    return {
+        "mlp_step": 16 * S + masks + feat + dz + wlast + masks,
+        "wgrad_hidden": S * elem * (hidden[0] + hidden[0]) if n_h > 1 else 0,
+        "wgrad_l0": S * elem * (Kp0 + hidden[0]),
+    }
+
+
+def pmc_traffic(cfg, precision, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py --traffic)."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))[f"{cfg}/{precision}"]
+        e = d[kernel]
+        return e["hbm_read_bytes"] + e["hbm_write_bytes"], d["source"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def make_opt(cfg, precision, B_total):
     import options
     from util import EasyDict as edict
@@ -214,6 +243,7 @@ def main():
         "wgrad_hidden": S * 2 * hidden[0] * hidden[0],
         "wgrad_l0": S * 2 * dims[0] * dims[1],
     }
+    kbytes = step_kernel_bytes(S, Kp0, hidden, 2 if args.precision == "bf16" else 4)
     per_kernel = {k: {"avg_ms": v[0] / v[1], "launches_per_step": v[1] / args.steps} for k, v in prof.items()}
     step_kernel_ms = sum(v[0] for v in prof.values()) / args.steps
     dom = max(prof.items(), key=lambda kv: kv[1][0])[0] if prof else None
@@ -221,10 +251,23 @@ def main():
     roof = None
     if dom in kflops:
         avg_s = prof[dom][0] / prof[dom][1] / 1e3
-        ach = kflops[dom] / avg_s
-        roof = {"kernel": dom, "bound": "mfma", "achieved": ach / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
-                "frac": ach / peak, "traffic": None,
-                "algorithmic_flops_per_launch": kflops[dom], "avg_launch_ms": avg_s * 1e3}
+        flops, nbytes = kflops[dom], kbytes.get(dom)
+        mfma = {"bound": "mfma", "achieved": flops / avg_s / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
+                "frac": flops / avg_s / peak, "algorithmic_flops_per_launch": flops}
+        hbm = None
+        if nbytes:
+            tr = pmc_traffic(args.config, args.precision, dom)
+            hbm = {"bound": "hbm", "achieved": nbytes / avg_s / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                   "frac": nbytes / avg_s / PEAK_HBM, "traffic": tr[0] if tr else None,
+                   "algorithmic_bytes_per_launch": nbytes}
+            if tr:
+                hbm["traffic_source"] = tr[1]
+        # the binding roof is the one with the larger lower bound on the kernel's time
+        if hbm and nbytes / PEAK_HBM >= flops / peak:
+            roof = dict(hbm, kernel=dom, avg_launch_ms=avg_s * 1e3, secondary=mfma)
+        else:
+            roof = dict(mfma, kernel=dom, avg_launch_ms=avg_s * 1e3, traffic=hbm["traffic"] if hbm else None,
+                        secondary=hbm)
     ms = elapsed / args.steps * 1e3
     value = world * px_local / (elapsed / args.steps)
     F = flops_per_px(dims)

@@ -15,6 +15,8 @@
 // 512 threads = 8 waves as 4 (rows) x 2 (cols); each wave owns RT x CT accumulator tiles.
 #include "marf_args.h"
 
+#include <cstdlib>
+
 namespace marf {
 
 struct WgArgs {
@@ -187,6 +189,168 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
     }
 }
 
+// ---- bf16, 256 output rows: LDS-DMA ring
+// The same product with the operands streamed HBM -> LDS by global_load_lds_dwordx4 into an
+// NBUF-deep ring of SP-pixel stages, NBUF-2 stages in flight behind the one being consumed (the
+// register-staged kernel above keeps one stage in flight; at one 8-wave block per CU the HBM
+// stream needs more bytes in flight than that).  LDS-DMA writes lane-linear 1 KB per wave
+// instruction, so the 512-B operand rows are unpadded and bank conflicts of the transposed reads are
+// avoided by an XOR swizzle of the 16-B chunks, applied on the global source address:
+// LDS chunk p of row r holds global chunk p ^ 4 (r & 3).  The ring spans the barriers: each thread
+// retires its own stage with a counted vmcnt, then a raw s_barrier (no __syncthreads: its fence
+// would drain every DMA in flight) publishes the stage to all waves.
+// Issued as inline asm: hipcc tracks its own builtin LDS-DMA and waits vmcnt(0) before the next
+// ds_read of the same LDS array, which would drain the ring; the asm form is outside its
+// bookkeeping, and the kernel counts completion itself.  lds: wave-uniform LDS byte address.
+MARF_DEV void glds16(const char* src, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
+}
+
+MARF_DEV int swz(int r, int c) {  // byte offset of bf16 element (r, c) in a 256-wide swizzled stage
+    return r * 512 + ((((c >> 3) ^ (4 * (r & 3)))) << 4) + (c & 7) * 2;
+}
+
+template <int N>
+MARF_DEV void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// KF = feat row width (bf16): 256 (hidden layers, swizzled like dz) or 96 (layer 0 at L = 16:
+// 192-B rows, the stage is one contiguous block copied linearly; rows r..r+3 of a transposed read
+// sit 0/192/384/576 B apart, i.e. in four distinct 64-B bank groups, so no swizzle is needed).
+template <int KF>
+MARF_DEV int foff(int r, int c) {
+    if constexpr (KF == 256) return swz(r, c);
+    else return r * (KF * 2) + c * 2;
+}
+
+template <int NBUF, int SP, int KF>
+__global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
+    static_assert(KF == 256 || KF == 96, "feat width");
+    constexpr int WR = KF == 256 ? 4 : 8, WC = 8 / WR;  // wave grid over the 256 x KF output
+    constexpr int RT = 256 / 32 / WR, CT = KF / 32 / WC;
+    constexpr int ZB = SP * 512;                 // bytes of the dz stage (SP rows x 256 bf16)
+    constexpr int FB = SP * KF * 2;              // bytes of the feat stage
+    constexpr int NGZ = ZB / 8192;               // DMA instructions per wave and stage (1 KB each)
+    constexpr int NGF = (FB + 8191) / 8192;      // (feat: the last round may be partly idle)
+    static_assert(NGZ * 8192 == ZB && FB % 1024 == 0 && NBUF >= 2 && NBUF <= 5, "stage shape");
+    constexpr int PER_ST = NGZ + NGF;            // vmcnt units per stage (the same on every wave)
+    constexpr int STB = ZB + FB;                 // bytes of one ring slot
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave / WC, wc = wave % WC;
+    const long long s_begin = (long long)blockIdx.x * a.chunk;
+    const long long s_end = min(s_begin + a.chunk, a.S);
+    const int n_st = s_end > s_begin ? (int)((s_end - s_begin) / SP) : 0;  // host: multiples of SP
+    const bool do_bias = a.bpartial != nullptr;
+    const char* dz = reinterpret_cast<const char*>(a.dz);
+    const char* ft = reinterpret_cast<const char*>(a.feat);
+    const size_t ldzb = (size_t)a.ldz * 2, ldfb = (size_t)a.ldf * 2;
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    const unsigned junk = lds0 + NBUF * STB;     // 1 KB sink for the idle feat rounds
+    auto issue = [&](int st) {
+        const unsigned buf = lds0 + (st % NBUF) * STB;
+        const long long row0 = s_begin + (long long)st * SP;
+#pragma unroll
+        for (int q = 0; q < NGZ; ++q) {
+            const int seg = q * 8 + wave;         // 1 KB = 2 rows per wave instruction
+            const int r = seg * 2 + (lane >> 5);
+            const int c16 = (lane & 31) ^ (4 * (r & 3));
+            glds16(dz + (size_t)(row0 + r) * ldzb + c16 * 16, __builtin_amdgcn_readfirstlane(buf + seg * 1024));
+        }
+#pragma unroll
+        for (int q = 0; q < NGF; ++q) {
+            const int seg = q * 8 + wave;
+            if constexpr (KF == 256) {
+                const int r = seg * 2 + (lane >> 5);
+                const int c16 = (lane & 31) ^ (4 * (r & 3));
+                glds16(ft + (size_t)(row0 + r) * ldfb + c16 * 16, __builtin_amdgcn_readfirstlane(buf + ZB + seg * 1024));
+            } else {
+                // rows are contiguous (ldf == KF): the stage is one linear block
+                const bool real = seg * 1024 < FB;
+                const char* src = ft + (size_t)row0 * ldfb + (real ? seg * 1024 : 0) + lane * 16;
+                glds16(src, __builtin_amdgcn_readfirstlane(real ? buf + ZB + seg * 1024 : junk));
+            }
+        }
+    };
+
+    f32x16 acc[RT][CT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) acc[i][j] = (f32x16){};
+    float bsum = 0.f;
+
+    for (int st = 0; st < NBUF - 1 && st < n_st; ++st) issue(st);
+    const int g = lane >> 4, gi = lane & 15, q4 = gi >> 2, p4 = gi & 3;
+    for (int st = 0; st < n_st; ++st) {
+        const int ahead = min(NBUF - 2, n_st - 1 - st);  // stages issued after st, still in flight
+        if (ahead >= 3) wait_vm<3 * PER_ST>();
+        else if (ahead == 2) wait_vm<2 * PER_ST>();
+        else if (ahead == 1) wait_vm<PER_ST>();
+        else wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // every wave is past its reads of buffer (st - 1) % NBUF: refill it
+        if (st + NBUF - 1 < n_st) issue(st + NBUF - 1);
+
+        const char* tz = smem + (st % NBUF) * STB;
+        const char* tf = tz + ZB;
+        if (do_bias) {
+            const int c = threadIdx.x & 255;
+#pragma unroll
+            for (int r = 0; r < SP; r += 2) {
+                const int rr = r + (threadIdx.x >> 8);
+                bsum += bf2f(*reinterpret_cast<const u16*>(tz + swz(rr, c)));
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < SP; ks += 16) {
+            const int r0 = ks + 8 * (g >> 1) + q4;  // rows r0 and r0 + 4 (same r & 3)
+            PrecBF16::frag af[RT], bf[CT];
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                const u16* base = reinterpret_cast<const u16*>(tz + swz(r0, (wr * RT + i) * 32 + 16 * (g & 1) + 4 * p4));
+                i16x4 v[2] = {tr_read(base), tr_read(base + 4 * 256)};
+                af[i] = *reinterpret_cast<bf16x8*>(v);
+            }
+#pragma unroll
+            for (int j = 0; j < CT; ++j) {
+                const u16* base = reinterpret_cast<const u16*>(tf + foff<KF>(r0, (wc * CT + j) * 32 + 16 * (g & 1) + 4 * p4));
+                i16x4 v[2] = {tr_read(base), tr_read(base + 4 * KF)};
+                bf[j] = *reinterpret_cast<bf16x8*>(v);
+            }
+#pragma unroll
+            for (int i = 0; i < RT; ++i)
+#pragma unroll
+                for (int j = 0; j < CT; ++j) acc[i][j] = PrecBF16::mma32(af[i], bf[j], acc[i][j]);
+        }
+    }
+
+    float* out = a.partial + (size_t)blockIdx.x * a.M * a.K;
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) {
+            const int k = (wc * CT + j) * 32 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) out[(size_t)((wr * RT + i) * 32 + acc_row(lane, r)) * a.K + k] = acc[i][j][r];
+        }
+    if (do_bias) {
+        __syncthreads();  // all DMA retired (the last iteration waited vmcnt(0)) and all reads done
+        float* bs = reinterpret_cast<float*>(smem);
+        bs[threadIdx.x] = bsum;
+        __syncthreads();
+        if (threadIdx.x < 256) a.bpartial[(size_t)blockIdx.x * a.M + threadIdx.x] = bs[threadIdx.x] + bs[threadIdx.x + 256];
+    }
+}
+
 // Last layer (3 outputs): dW[c][k] = sum_px g[px][c] feat[px][k], db[c] = sum_px g[px][c].
 // Bandwidth-bound (reads feat_{n-1} once): each thread owns VEC consecutive features (one 16-byte
 // load per pixel row) and a pixel lane; a wave covers whole rows so every load instruction is
@@ -346,6 +510,25 @@ static hipError_t launch_wg(const WgArgs& a, int n_chunks, int n_oblk, hipStream
     return hipGetLastError();
 }
 
+static bool wgrad_dma_enabled() {
+    const char* e = getenv("MARF_WGRAD_DMA");  // A/B switch (read per launch): 0 = register-staged kernel
+    return !(e && e[0] == '0');
+}
+
+template <int KF>
+static hipError_t launch_wg_dma(const WgArgs& a, int n_chunks, hipStream_t s) {
+    constexpr int NBUF = 4, SP = 32;
+    const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + 1024;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_wgrad_dma<NBUF, SP, KF>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_wgrad_dma<NBUF, SP, KF>), dim3(n_chunks), dim3(512), lds, s, a);
+    return hipGetLastError();
+}
+
 // Picks the output-block shape for an M x K weight gradient: 256x256 (2x4 tiles per wave),
 // 256x64 (2x1) or 128x64 (1x1).
 hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
@@ -370,6 +553,10 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
     int nr = (M + BM - 1) / BM, nc = (K + BN - 1) / BN;
     a.n_oblk_c = nc;
     if (dtype == 1) {
+        // LDS-DMA ring: 256-wide dz with a 256-wide (hidden) or 96-wide (layer 0, L = 16) feat
+        const bool dma = M == 256 && ldz == 256 && S % 32 == 0 && chunk % 32 == 0 && wgrad_dma_enabled();
+        if (dma && K == 256 && ldf == 256) return launch_wg_dma<256>(a, n_chunks, s);
+        if (dma && K == 96 && ldf == 96) return launch_wg_dma<96>(a, n_chunks, s);
         if (cfg == 0) return launch_wg<PrecBF16, 2, 4>(a, n_chunks, nr * nc, s);
         if (cfg == 3) return launch_wg<PrecBF16, 2, 2>(a, n_chunks, nr * nc, s);
         if (cfg == 1) return launch_wg<PrecBF16, 2, 1>(a, n_chunks, nr * nc, s);

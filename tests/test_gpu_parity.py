@@ -478,11 +478,21 @@ def test_fused_step_c3_linearity_and_determinism(tmp_path):
     assert all(torch.equal(a, b) for a, b in zip(g1, g2)) and torch.equal(w1, w2)
     assert all(torch.equal(2 * a, b) for a, b in zip(g1, g3)) and torch.equal(2 * w1, w3)
     assert all(torch.isfinite(a).all() for a in g1) and torch.isfinite(w1).all()
+    # the LDS-DMA hidden-layer weight-gradient kernel sums in the same pixel order as the
+    # register-staged one: bit-identical gradients
+    os.environ["MARF_WGRAD_DMA"] = "0"
+    try:
+        l4, g4, w4 = run(1.0)
+    finally:
+        del os.environ["MARF_WGRAD_DMA"]
+    assert l4 == l1 and torch.equal(w4, w1)
+    for i, (a, b) in enumerate(zip(g1, g4)):
+        assert torch.equal(a, b), (i, (a - b).abs().max().item())
 
 
 def test_bf16_gradients_vs_fp32_c3_width(tmp_path):
-    """C3 widths (L=16, 4 x 256 hidden: the LDS-DMA weight-gradient kernel and the 128-pixel
-    tiles): bf16 MLP gradients against the fp32 path from the same state (cosine >= 0.995 and
+    """C3 widths (L=16, 4 x 256 hidden: the LDS-DMA hidden-layer weight-gradient kernel and the
+    128-pixel tiles): bf16 MLP gradients against the fp32 path from the same state (cosine >= 0.995 and
     max error <= 5e-2 of the max per tensor: bf16 features / dz, measured 0.998 / 3.5e-2 on the
     layer-0 weight); warp gradient cosine >= 0.99 against fp32 and <= 2e-2 against the
     separate-kernel bf16 path."""
