@@ -1,6 +1,7 @@
 """Build libmarf.so (all HIP sources, gfx950 only) in-tree: lib/libmarf.so.
 
     python build_lib.py [--force]
+    python build_lib.py --variant libmarf_<name>.so "<extra hipcc flags>"   (A/B variants, MARF_LIB=...)
 
 The library is rebuilt when any source under csrc/ or include/ is newer than it.
 """
@@ -54,4 +55,8 @@ def _compile(lib_path, extra, verbose):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, stamps="--stamps" in sys.argv)
+    if "--variant" in sys.argv:  # A/B builds: --variant libmarf_<x>.so "-DFLAG=..." (loaded via MARF_LIB)
+        i = sys.argv.index("--variant")
+        _compile(os.path.join(HERE, "lib", sys.argv[i + 1]), sys.argv[i + 2].split() if len(sys.argv) > i + 2 else [], True)
+    else:
+        build(force="--force" in sys.argv, stamps="--stamps" in sys.argv)

@@ -237,7 +237,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     constexpr int FB = SP * KF * 2;              // bytes of the feat stage
     constexpr int NGZ = ZB / 8192;               // DMA instructions per wave and stage (1 KB each)
     constexpr int NGF = (FB + 8191) / 8192;      // (feat: the last round may be partly idle)
-    static_assert(NGZ * 8192 == ZB && FB % 1024 == 0 && NBUF >= 2 && NBUF <= 5, "stage shape");
+    static_assert(NGZ * 8192 == ZB && FB % 1024 == 0 && NBUF >= 2 && NBUF <= 6, "stage shape");
     constexpr int PER_ST = NGZ + NGF;            // vmcnt units per stage (the same on every wave)
     constexpr int STB = ZB + FB;                 // bytes of one ring slot
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -290,7 +290,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     const int g = lane >> 4, gi = lane & 15, q4 = gi >> 2, p4 = gi & 3;
     for (int st = 0; st < n_st; ++st) {
         const int ahead = min(NBUF - 2, n_st - 1 - st);  // stages issued after st, still in flight
-        if (ahead >= 3) wait_vm<3 * PER_ST>();
+        if (ahead >= 4) wait_vm<4 * PER_ST>();
+        else if (ahead == 3) wait_vm<3 * PER_ST>();
         else if (ahead == 2) wait_vm<2 * PER_ST>();
         else if (ahead == 1) wait_vm<PER_ST>();
         else wait_vm<0>();
@@ -515,10 +516,18 @@ static bool wgrad_dma_enabled() {
     return !(e && e[0] == '0');
 }
 
+#ifndef MARF_WG_NBUF_H
+#define MARF_WG_NBUF_H 4
+#endif
+#ifndef MARF_WG_NBUF_0
+#define MARF_WG_NBUF_0 4
+#endif
+
 template <int KF>
 static hipError_t launch_wg_dma(const WgArgs& a, int n_chunks, hipStream_t s) {
-    constexpr int NBUF = 4, SP = 32;
-    const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + 1024;
+    constexpr int SP = 32;
+    constexpr int NBUF = KF == 256 ? MARF_WG_NBUF_H : MARF_WG_NBUF_0;  // ring depth within 160 KB of LDS
+    const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024);
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)k_wgrad_dma<NBUF, SP, KF>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -71,6 +71,8 @@ if "--traffic" in sys.argv:
         name = None
         if k.startswith("k_mlp_step"):
             name = "mlp_step"
+        elif k.startswith("k_wgrad_dma<"):
+            name = "wgrad_hidden" if k.rstrip(">").endswith("256") else "wgrad_l0"
         elif k.startswith("k_wgrad<"):
             name = "wgrad_hidden" if ", 2, 4" in k else "wgrad_l0"
         if name and "hbm_read_bytes" in r and "hbm_write_bytes" in r:
