@@ -49,7 +49,7 @@ def flops_per_px(dims):
 def step_kernel_bytes(S, Kp0, hidden, elem):
     """Algorithmic HBM bytes per launch of the store-activations decomposition (each value moved
     once): the fused step reads targets + masks (16 B/px, fp32) and its own ReLU-mask records back,
-    and writes every saved layer input feat_0..feat_{n-2}, every dz_1..dz_{n-1} (elem bytes per
+    and writes rgb (12 B/px), every saved layer input feat_0..feat_{n-2}, every dz_1..dz_{n-1} (elem bytes per
     feature), the ReLU-mask records (1 bit per hidden feature) and the per-tile last-layer gradient
     partials; each weight-gradient kernel reads dz_{l+1} and feat_l once."""
     n_h = len(hidden)
@@ -58,7 +58,7 @@ def step_kernel_bytes(S, Kp0, hidden, elem):
     dz = S * elem * sum(hidden)
     wlast = (S // 128) * 4 * 3 * hidden[-1]
     return {
-        "mlp_step": 16 * S + masks + feat + dz + wlast + masks,
+        "mlp_step": 16 * S + 12 * S + masks + feat + dz + wlast + masks,
         "wgrad_hidden": S * elem * (hidden[0] + hidden[0]) if n_h > 1 else 0,
         "wgrad_l0": S * elem * (Kp0 + hidden[0]),
     }
