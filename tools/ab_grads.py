@@ -1,0 +1,62 @@
+"""Dump the gradients of one fused bf16 training step at C3 widths (8 patches) so two library
+builds can be compared bit for bit:  MARF_LIB=<lib> python tools/ab_grads.py out.npz
+then  python tools/ab_grads.py --compare a.npz b.npz"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def dump(path):
+    import torch
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "masking-bundle-adjusting-neural-radiance-fields_amd"))
+    import bench
+    from model import planar
+    from util import EasyDict as edict
+    dev = torch.device("cuda", 0)
+    B = 8
+    opt = bench.make_opt("c3", "bf16", B)
+    opt.device = str(dev)
+    torch.manual_seed(3)
+    graph = planar.Graph(opt).to(dev)
+    graph.neural_image.progress.data.fill_(0.2)
+    rgb, mask, warp = bench.synthetic_inputs(B, opt.patch_H, opt.patch_W, dev)
+    with torch.no_grad():
+        graph.warp_param.weight.copy_(warp)
+    graph.need_edges = False
+    var = edict(images=edict(rgb=rgb, masks=mask, masks_eroded=mask, edges=None))
+    out = {}
+    for it in range(2):
+        for p in graph.parameters():
+            p.grad = None
+        v = graph.forward(var, mode="train")
+        loss = graph.compute_loss(v, mode="train").rgb
+        loss.backward()
+        out[f"loss{it}"] = np.array([float(loss)])
+        out[f"rgb{it}"] = v.rgb_prediction.detach().cpu().numpy()
+        for n, p in graph.named_parameters():
+            if p.grad is not None:
+                out[f"{n}.grad{it}"] = p.grad.cpu().numpy()
+    np.savez(path, **out)
+    print("wrote", path, len(out))
+
+
+def compare(a, b):
+    A, Bz = np.load(a), np.load(b)
+    bad = 0
+    for k in A.files:
+        same = np.array_equal(A[k], Bz[k])
+        if not same:
+            bad += 1
+            print(f"{k}: max |diff| {np.abs(A[k] - Bz[k]).max():.3e}")
+    print("identical" if bad == 0 else f"{bad} arrays differ")
+    return bad
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "--compare":
+        sys.exit(1 if compare(sys.argv[2], sys.argv[3]) else 0)
+    dump(sys.argv[1])
