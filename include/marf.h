@@ -125,6 +125,11 @@ int marf_masked_mse(const float* d_pred, const float* d_gt, const float* d_mask,
 int marf_masked_mse_backward(const float* d_pred, const float* d_gt, const float* d_mask, int B, int Np,
                              const float* d_denom, const float* d_gout, float* d_dpred, void* stream);
 
+/* ---- Edge maps (inputs.compute_edges, reference inputs.py:50-67: cv2.Sobel 3x3 CV_64F in x and y,
+ * magnitude, cv2.GaussianBlur 5x5 sigma 0, BORDER_REFLECT_101), per channel image on the device.
+ * d_img [n_img][H][W] fp32 -> d_out [n_img][H][W] fp64. */
+int marf_edge_map(const float* d_img, int n_img, int H, int W, double* d_out, void* stream);
+
 /* ---- Adam (torch.optim.Adam, model/planar.py:98-99): one parameter segment, step >= 1.
  * d_grad_scale: optional device scalar multiplying the gradient (NULL = 1). */
 int marf_adam_step(float* d_p, const float* d_g, float* d_m, float* d_v, long long n, double lr, double beta1,

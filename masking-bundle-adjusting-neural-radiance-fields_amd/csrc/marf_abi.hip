@@ -644,6 +644,15 @@ int marf_masked_mse_backward(const float* d_pred, const float* d_gt, const float
     return MARF_OK;
 }
 
+int marf_edge_map(const float* d_img, int n_img, int H, int W, double* d_out, void* stream) {
+    if (n_img < 0 || H <= 0 || W <= 0 || (n_img > 0 && (!d_img || !d_out))) return fail(MARF_ERR_INVALID, "edge_map: bad args");
+    if (n_img > 65535) return fail(MARF_ERR_INVALID, "edge_map: more than 65535 channel images");
+    if (n_img == 0) return MARF_OK;
+    MarfProfScope ps("edge_map", (hipStream_t)stream);
+    HIPCHK(marf_launch_edge_map(d_img, d_out, n_img, H, W, (hipStream_t)stream), "edge_map");
+    return MARF_OK;
+}
+
 int marf_adam_step(float* d_p, const float* d_g, float* d_m, float* d_v, long long n, double lr, double beta1,
                    double beta2, double eps, long long step, const float* d_grad_scale, void* stream) {
     if (n < 0 || step < 1 || (n > 0 && (!d_p || !d_g || !d_m || !d_v))) return fail(MARF_ERR_INVALID, "adam: bad args");

@@ -55,39 +55,12 @@ def load_single_image(fp, device, mode="RGB"):
     return _to_tensor(np.array(im, dtype=np.uint8, copy=True)).to(device)
 
 
-def _corr1d(a, k, axis):
-    from scipy.ndimage import correlate1d
-    return correlate1d(a, k, axis=axis, mode="mirror")  # scipy 'mirror' == cv2 BORDER_REFLECT_101
-
-
-def _gauss5():
-    # cv2.getGaussianKernel(5, 0): sigma = 0.3*((5-1)*0.5 - 1) + 0.8
-    sigma = 0.3 * ((5 - 1) * 0.5 - 1) + 0.8
-    x = np.arange(5) - 2
-    k = np.exp(-(x * x) / (2 * sigma * sigma))
-    return k / k.sum()
-
-
-def edge_map(img_hwc):
-    """Sobel magnitude + Gaussian blur of one HxWxC image (float64 result, channels kept)."""
-    a = np.asarray(img_hwc, np.float64)
-    d = np.array([-1.0, 0.0, 1.0])
-    s = np.array([1.0, 2.0, 1.0])
-    sx = _corr1d(_corr1d(a, d, 1), s, 0)
-    sy = _corr1d(_corr1d(a, s, 1), d, 0)
-    m = np.sqrt(sx * sx + sy * sy)
-    g = _gauss5()
-    return _corr1d(_corr1d(m, g, 1), g, 0)
-
-
 def compute_edges(images_tensor, device):
-    """[B, C, H, W] -> [B, C, H, W] float64 edge images (C == 1 kept as one channel)."""
-    out = []
-    for image in images_tensor:
-        i = image.detach().cpu().numpy().transpose(1, 2, 0)
-        e = edge_map(i)
-        out.append(_to_tensor(e).to(device))
-    return torch.stack(out)
+    """inputs.compute_edges (reference inputs.py:50-67): [B, C, H, W] -> [B, C, H, W] float64 edge
+    images (cv2.Sobel 3x3 CV_64F x / y, magnitude, cv2.GaussianBlur 5x5 sigma 0, reflect-101), in one
+    HIP launch on the device (marf_edge_map); C == 1 stays one channel, as cv2 + to_tensor give."""
+    import marf_hip
+    return marf_hip.edge_map(images_tensor.to(device))
 
 
 def erode_images(images_tensor, device, kernel=(5, 5)):

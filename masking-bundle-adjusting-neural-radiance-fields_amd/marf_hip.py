@@ -53,6 +53,7 @@ _SIGS = {
     "marf_step_backward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                                     _c_vp]),
     "marf_mse_workspace_bytes": (_c_sz, []),
+    "marf_edge_map": (_c_int, [_c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp]),
     "marf_masked_mse": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_masked_mse_backward": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_adam_step": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_ll, _c_dbl, _c_dbl, _c_dbl, _c_dbl, _c_ll, _c_vp,
@@ -580,6 +581,19 @@ def mse_stats(pred_bn3, gt_b3n, mask_b1n=None):
     ws = _BUFS.get("mse_ws", lib().marf_mse_workspace_bytes(), pred.device)
     _check(lib().marf_masked_mse(_ptr(pred), _ptr(gt), _ptr(mask), pred.shape[0], pred.shape[1], None, _ptr(out),
                                  _ptr(ws), _stream(pred)))
+    return out
+
+
+# ====================================================================== edge maps
+
+def edge_map(images):
+    """inputs.compute_edges (reference inputs.py:50-67) on the device: [B, C, H, W] (any float layout)
+    -> [B, C, H, W] float64 Sobel-magnitude edge maps, Gaussian-blurred (cv2 semantics)."""
+    _dev(images, "images")
+    x = images.detach().to(torch.float32).contiguous()
+    B, C, H, W = x.shape
+    out = torch.empty((B, C, H, W), dtype=torch.float64, device=x.device)
+    _check(lib().marf_edge_map(_ptr(x), B * C, H, W, _ptr(out), _stream(x)))
     return out
 
 

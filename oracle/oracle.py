@@ -293,3 +293,50 @@ class PlanarStep:
         if cfg.get("fix_first", True):
             self.warp[0] = 0
         return dict(loss_rgb=loss, grads=grads, dh=dh, rgb=fw["rgb"], dH=dH)
+
+
+# ---------------------------------------------------------------- edge stencil (SURVEY §8f row 2)
+# inputs.compute_edges (reference inputs.py:50-67): per image, cv2.Sobel(i, CV_64F, 1, 0, ksize=3)
+# and (0, 1), magnitude sqrt(sx^2 + sy^2), cv2.GaussianBlur(., (5, 5), 0).  cv2 is absent here, so
+# this restates OpenCV's documented semantics (parity unpinned against cv2 itself):
+#   * default border BORDER_REFLECT_101 (…dcb|abcd|cba…) for both filters;
+#   * Sobel ksize 3 = separable [-1, 0, 1] (derivative) x [1, 2, 1] (smoothing);
+#   * GaussianBlur ksize 5 with sigma 0 takes OpenCV's fixed small-kernel table
+#     [1, 4, 6, 4, 1] / 16 (getGaussianKernel: sigma <= 0 and odd ksize <= 7), row pass then
+#     column pass.
+# Evaluation order (fp64): Sobel sums of fp32 inputs are exact in fp64; the blur accumulates left to
+# right, ((((g0 m0 + g1 m1) + g2 m2) + g3 m3) + g4 m4), which the HIP kernel follows.
+EDGE_GAUSS5 = np.array([0.0625, 0.25, 0.375, 0.25, 0.0625], np.float64)
+
+
+def _reflect101(idx, n):
+    idx = np.asarray(idx)
+    if n == 1:
+        return np.zeros_like(idx)
+    period = 2 * n - 2
+    idx = np.abs(idx) % period
+    return np.where(idx >= n, period - idx, idx)
+
+
+def edge_map(img):
+    """[N, H, W] float32 images -> [N, H, W] float64 edge maps (inputs.compute_edges per channel)."""
+    a = np.asarray(img, np.float32).astype(np.float64)
+    N, H, W = a.shape
+    ry = _reflect101(np.arange(-1, H + 1), H)
+    rx = _reflect101(np.arange(-1, W + 1), W)
+    e = a[:, ry][:, :, rx]                     # [N, H+2, W+2]
+    c = e[:, 1:-1]
+    up, dn = e[:, :-2], e[:, 2:]
+    sx = ((up[:, :, 2:] - up[:, :, :-2]) + 2.0 * (c[:, :, 2:] - c[:, :, :-2])) + (dn[:, :, 2:] - dn[:, :, :-2])
+    sy = ((dn[:, :, :-2] - up[:, :, :-2]) + 2.0 * (dn[:, :, 1:-1] - up[:, :, 1:-1])) + (dn[:, :, 2:] - up[:, :, 2:])
+    m = np.sqrt(sx * sx + sy * sy)
+    g = EDGE_GAUSS5
+    mx = m[:, :, _reflect101(np.arange(-2, W + 2), W)]
+    r = g[0] * mx[:, :, 0:W]
+    for j in range(1, 5):
+        r = r + g[j] * mx[:, :, j:j + W]
+    ry5 = r[:, _reflect101(np.arange(-2, H + 2), H)]
+    out = g[0] * ry5[:, 0:H]
+    for j in range(1, 5):
+        out = out + g[j] * ry5[:, j:j + H]
+    return out

@@ -541,6 +541,26 @@ def test_bf16_gradients_vs_fp32_c3_width(tmp_path):
     assert float((res["bf16"][1] - ws).abs().max() / ws.abs().max()) <= 2e-2
 
 
+# ------------------------------------------------------------------------ edge maps (inputs.py:50-67)
+
+@pytest.mark.parametrize("shape", [(2, 3, 37, 53), (1, 1, 16, 16), (3, 3, 180, 240), (1, 1, 5, 7), (1, 2, 1, 9)])
+def test_edge_map_matches_oracle(shape):
+    """HIP edge stencil vs the oracle restatement of cv2 Sobel + magnitude + GaussianBlur(5x5, 0):
+    same fp64 evaluation order, equal to 1 ulp-level (<= 1e-15 relative to the map's max)."""
+    _need_gpu()
+    import inputs
+    rng = np.random.default_rng(sum(shape))
+    img = rng.random(shape).astype(np.float32)
+    got = inputs.compute_edges(t(img), DEV)
+    assert got.dtype == torch.float64 and tuple(got.shape) == shape
+    ref = oracle.edge_map(img.reshape(-1, shape[2], shape[3])).reshape(shape)
+    g = got.cpu().numpy()
+    np.testing.assert_allclose(g, ref, rtol=0, atol=1e-15 * max(1.0, np.abs(ref).max()))
+    # a non-contiguous [B, 3, h, w] view (rgb_prediction_map is one) gives the same maps
+    view = t(img.transpose(0, 2, 3, 1).copy()).permute(0, 3, 1, 2)
+    np.testing.assert_array_equal(inputs.compute_edges(view, DEV).cpu().numpy(), g)
+
+
 # ------------------------------------------------------------------------ end-to-end (3000 steps)
 
 # Reference run (SURVEY.md §6: the reference's Graph / Adam imported here through the stub harness,

@@ -158,3 +158,33 @@ def test_c1_init_and_first_steps(golden):
         losses.append(st.step()["loss_rgb"])
     np.testing.assert_allclose(losses, g["loss"], rtol=1e-5)
     np.testing.assert_allclose(st.warp, g["warp_traj"][-1], atol=1e-6)
+
+
+# ---------------------------------------------------------------- edge stencil (inputs.py:50-67)
+# cv2 is absent here and the reference's edge term carries no gradient, so no fixture
+# holds its output: the restatement is pinned by OpenCV's documented kernels and borders through
+# known answers below ("parity unpinned" against cv2 itself).
+
+def test_edge_reflect101_indices():
+    # BORDER_REFLECT_101: gfedcb|abcdefgh|gfedcba
+    idx = oracle._reflect101(np.arange(-3, 11), 8)
+    assert idx.tolist() == [3, 2, 1, 0, 1, 2, 3, 4, 5, 6, 7, 6, 5, 4]
+
+
+def test_edge_gaussian_is_opencv_small_table():
+    # getGaussianKernel(5, sigma <= 0) = fixed table [1, 4, 6, 4, 1] / 16
+    assert oracle.EDGE_GAUSS5.tolist() == [1 / 16, 4 / 16, 6 / 16, 4 / 16, 1 / 16]
+
+
+def test_edge_known_answers():
+    assert np.abs(oracle.edge_map(np.full((1, 9, 11), 0.3, np.float32))).max() == 0.0
+    # horizontal ramp 0.5 x: Sobel x = (1 + 2 + 1) * (2 * 0.5) = 4 inside, 0 on the reflected
+    # border column; blur of the border: (1 + 4 + 0 + 4 + 1) / 16 * 4 = 2.5, next (4+6+4+1+1 * 0)/16 * 4
+    ramp = np.broadcast_to(np.arange(11, dtype=np.float32) * 0.5, (9, 11))[None].copy()
+    e = oracle.edge_map(ramp)
+    np.testing.assert_array_equal(e[0, :, 3:8], 4.0)
+    assert e[0, 4, 0] == 2.5 and e[0, 4, 1] == 3.0 and e[0, 4, 2] == 3.75
+    np.testing.assert_array_equal(e[0, :, 0], 2.5)  # constant down the column (vertical smoothing)
+    # transpose symmetry: the vertical ramp gives the transposed map
+    np.testing.assert_array_equal(oracle.edge_map(ramp.transpose(0, 2, 1).copy())[0], e[0].T)
+    assert e.dtype == np.float64
