@@ -130,6 +130,10 @@ int marf_masked_mse_backward(const float* d_pred, const float* d_gt, const float
  * d_img [n_img][H][W] fp32 -> d_out [n_img][H][W] fp64. */
 int marf_edge_map(const float* d_img, int n_img, int H, int W, double* d_out, void* stream);
 
+/* ---- Mask erosion (erode_images, reference inputs.py:71-85: cv2.erode with a kh x kw MORPH_RECT
+ * element, default anchor and border).  d_img [n_img][H][W] fp32 -> d_out (a different buffer). */
+int marf_erode_rect(const float* d_img, int n_img, int H, int W, int kh, int kw, float* d_out, void* stream);
+
 /* ---- Adam (torch.optim.Adam, model/planar.py:98-99): one parameter segment, step >= 1.
  * d_grad_scale: optional device scalar multiplying the gradient (NULL = 1). */
 int marf_adam_step(float* d_p, const float* d_g, float* d_m, float* d_v, long long n, double lr, double beta1,

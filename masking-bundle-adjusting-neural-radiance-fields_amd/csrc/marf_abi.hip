@@ -653,6 +653,16 @@ int marf_edge_map(const float* d_img, int n_img, int H, int W, double* d_out, vo
     return MARF_OK;
 }
 
+int marf_erode_rect(const float* d_img, int n_img, int H, int W, int kh, int kw, float* d_out, void* stream) {
+    if (n_img < 0 || H <= 0 || W <= 0 || kh <= 0 || kw <= 0 || (n_img > 0 && (!d_img || !d_out)))
+        return fail(MARF_ERR_INVALID, "erode_rect: bad args");
+    if (n_img > 65535) return fail(MARF_ERR_INVALID, "erode_rect: more than 65535 channel images");
+    if (d_img == d_out) return fail(MARF_ERR_INVALID, "erode_rect: in-place erosion is not supported");
+    if (n_img == 0) return MARF_OK;
+    HIPCHK(marf_launch_erode_rect(d_img, d_out, n_img, H, W, kh, kw, (hipStream_t)stream), "erode_rect");
+    return MARF_OK;
+}
+
 int marf_adam_step(float* d_p, const float* d_g, float* d_m, float* d_v, long long n, double lr, double beta1,
                    double beta2, double eps, long long step, const float* d_grad_scale, void* stream) {
     if (n < 0 || step < 1 || (n > 0 && (!d_p || !d_g || !d_m || !d_v))) return fail(MARF_ERR_INVALID, "adam: bad args");

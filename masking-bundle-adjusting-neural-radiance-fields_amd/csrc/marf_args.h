@@ -90,6 +90,7 @@ hipError_t marf_launch_mlp_step(const marf::StepArgs& a, int dtype, int TP, size
 hipError_t marf_launch_c2f_weights(const marf::C2fDev& c, int L, float* out, hipStream_t s);
 hipError_t marf_launch_loss_final(const double* part, int n, float* out, const float* denom_override, hipStream_t s);
 hipError_t marf_launch_edge_map(const float* in, double* out, int n_img, int H, int W, hipStream_t s);
+hipError_t marf_launch_erode_rect(const float* in, float* out, int n_img, int H, int W, int kh, int kw, hipStream_t s);
 hipError_t marf_launch_mse(const float* pred, const float* gt, const float* mask, int B, int Np, double* part,
                            float* out, const float* denom_override, hipStream_t s);
 hipError_t marf_launch_mse_bwd(const float* pred, const float* gt, const float* mask, int B, int Np,

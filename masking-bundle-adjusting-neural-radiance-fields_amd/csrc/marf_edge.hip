@@ -1,4 +1,4 @@
-// marf_edge.hip -- edge maps of the rendered patches and targets on the GPU.
+// marf_edge.hip -- edge maps and mask erosion on the GPU.
 //
 // inputs.compute_edges (reference inputs.py:50-67) runs per image on the host through cv2:
 // Sobel 3x3 (CV_64F) in x and y, magnitude, GaussianBlur 5x5 with sigma 0, BORDER_REFLECT_101.
@@ -61,9 +61,32 @@ __global__ __launch_bounds__(256) void k_edge_map(const float* __restrict__ in, 
     }
 }
 
+// erode_images (reference inputs.py:71-85): cv2.erode with a kh x kw MORPH_RECT element, anchor at
+// its centre (kw / 2, kh / 2), default border (constant +max for erosion: out-of-image taps never
+// win), i.e. the minimum over the in-image part of the window.  One thread per pixel; the window
+// reads are L1 hits.
+__global__ __launch_bounds__(256) void k_erode_rect(const float* __restrict__ in, float* __restrict__ out, int H, int W,
+                                                    int kh, int kw) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const float* img = in + (size_t)blockIdx.z * H * W;
+    const int ya = max(0, y - kh / 2), yb = min(H, y - kh / 2 + kh);
+    const int xa = max(0, x - kw / 2), xb = min(W, x - kw / 2 + kw);
+    float m = img[(size_t)y * W + x];
+    for (int yy = ya; yy < yb; ++yy)
+        for (int xx = xa; xx < xb; ++xx) m = fminf(m, img[(size_t)yy * W + xx]);
+    out[(size_t)blockIdx.z * H * W + (size_t)y * W + x] = m;
+}
+
 }  // namespace marf
 
 using namespace marf;
+
+hipError_t marf_launch_erode_rect(const float* in, float* out, int n_img, int H, int W, int kh, int kw, hipStream_t s) {
+    dim3 grid((W + 15) / 16, (H + 15) / 16, n_img);
+    hipLaunchKernelGGL(k_erode_rect, grid, dim3(256), 0, s, in, out, H, W, kh, kw);
+    return hipGetLastError();
+}
 
 hipError_t marf_launch_edge_map(const float* in, double* out, int n_img, int H, int W, hipStream_t s) {
     dim3 grid((W + 15) / 16, (H + 15) / 16, n_img);

@@ -64,13 +64,10 @@ def compute_edges(images_tensor, device):
 
 
 def erode_images(images_tensor, device, kernel=(5, 5)):
-    from scipy.ndimage import minimum_filter
-    out = []
-    for image in images_tensor:
-        i = image.detach().cpu().numpy().transpose(1, 2, 0)
-        e = minimum_filter(i, size=(kernel[1], kernel[0], 1), mode="nearest")
-        out.append(_to_tensor(e).to(device))
-    return torch.stack(out)
+    """erode_images (reference inputs.py:71-85): cv2.erode with a kernel = (width, height) MORPH_RECT
+    element, default anchor / border, per channel image; one HIP launch (marf_erode_rect)."""
+    import marf_hip
+    return marf_hip.erode_rect(images_tensor.to(device), kernel)
 
 
 def _normal_transform_pixel(height, width, eps=1e-14):

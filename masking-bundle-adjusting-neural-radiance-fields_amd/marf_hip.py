@@ -54,6 +54,7 @@ _SIGS = {
                                     _c_vp]),
     "marf_mse_workspace_bytes": (_c_sz, []),
     "marf_edge_map": (_c_int, [_c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp]),
+    "marf_erode_rect": (_c_int, [_c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_vp, _c_vp]),
     "marf_masked_mse": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_masked_mse_backward": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_adam_step": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_ll, _c_dbl, _c_dbl, _c_dbl, _c_dbl, _c_ll, _c_vp,
@@ -594,6 +595,17 @@ def edge_map(images):
     B, C, H, W = x.shape
     out = torch.empty((B, C, H, W), dtype=torch.float64, device=x.device)
     _check(lib().marf_edge_map(_ptr(x), B * C, H, W, _ptr(out), _stream(x)))
+    return out
+
+
+def erode_rect(images, kernel=(5, 5)):
+    """erode_images (reference inputs.py:71-85) on the device: [B, C, H, W] float -> float32 of the
+    same shape, cv2.erode with a kernel[0] (width) x kernel[1] (height) rectangle."""
+    _dev(images, "images")
+    x = images.detach().to(torch.float32).contiguous()
+    B, C, H, W = x.shape
+    out = torch.empty_like(x)
+    _check(lib().marf_erode_rect(_ptr(x), B * C, H, W, int(kernel[1]), int(kernel[0]), _ptr(out), _stream(x)))
     return out
 
 

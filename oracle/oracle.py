@@ -340,3 +340,18 @@ def edge_map(img):
     for j in range(1, 5):
         out = out + g[j] * ry5[:, j:j + H]
     return out
+
+
+def erode_rect(img, kh=5, kw=5):
+    """erode_images (reference inputs.py:71-85): cv2.erode with a kh x kw MORPH_RECT element, anchor
+    at its centre, default border (constant +max for erosion): min over the in-image window part.
+    [N, H, W] float32 -> float32."""
+    a = np.asarray(img, np.float32)
+    N, H, W = a.shape
+    pad = np.full((N, H + kh - 1, W + kw - 1), np.inf, np.float32)
+    pad[:, kh // 2:kh // 2 + H, kw // 2:kw // 2 + W] = a
+    out = np.full_like(a, np.inf)
+    for dy in range(kh):
+        for dx in range(kw):
+            out = np.minimum(out, pad[:, dy:dy + H, dx:dx + W])
+    return out

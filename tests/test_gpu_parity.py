@@ -561,6 +561,18 @@ def test_edge_map_matches_oracle(shape):
     np.testing.assert_array_equal(inputs.compute_edges(view, DEV).cpu().numpy(), g)
 
 
+@pytest.mark.parametrize("shape,kernel", [((2, 1, 37, 53), (5, 5)), ((1, 3, 16, 16), (5, 5)), ((1, 1, 7, 9), (3, 5))])
+def test_erode_matches_oracle(shape, kernel):
+    """HIP mask erosion vs the oracle restatement of cv2.erode(MORPH_RECT): exact."""
+    _need_gpu()
+    import inputs
+    rng = np.random.default_rng(7)
+    img = (rng.random(shape) < 0.9).astype(np.float32) * rng.random(shape).astype(np.float32)
+    got = inputs.erode_images(t(img), DEV, kernel=kernel).cpu().numpy()
+    ref = oracle.erode_rect(img.reshape(-1, shape[2], shape[3]), kh=kernel[1], kw=kernel[0]).reshape(shape)
+    np.testing.assert_array_equal(got, ref)
+
+
 # ------------------------------------------------------------------------ end-to-end (3000 steps)
 
 # Reference run (SURVEY.md §6: the reference's Graph / Adam imported here through the stub harness,

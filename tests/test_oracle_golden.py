@@ -188,3 +188,12 @@ def test_edge_known_answers():
     # transpose symmetry: the vertical ramp gives the transposed map
     np.testing.assert_array_equal(oracle.edge_map(ramp.transpose(0, 2, 1).copy())[0], e[0].T)
     assert e.dtype == np.float64
+
+
+def test_erode_known_answers():
+    m = np.ones((1, 9, 10), np.float32)
+    m[0, 4, 6] = 0.0
+    e = oracle.erode_rect(m)
+    # a single hole grows to the 5x5 square around it; the border itself is not eroded
+    assert (e[0] == 0).sum() == 25 and e[0, 2:7, 4:9].max() == 0.0
+    assert oracle.erode_rect(np.ones((1, 6, 6), np.float32)).min() == 1.0
