@@ -26,6 +26,7 @@ struct WgArgs {
     int ldz, ldf;      // row strides
     int M, K;          // output rows (<= ldz) and cols (<= ldf)
     int chunk;         // pixels per chunk (multiple of 64)
+    int n_chunks;
     int n_oblk_c;      // output blocks along K
     float* partial;    // [n_chunks][M][K]
     float* bpartial;   // [n_chunks][M] (bias), may be null
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
     }
 }
 
-// ---- bf16, 256 output rows: LDS-DMA ring
+// ---- bf16, 256 x 256 (or 256 x 96) output blocks: LDS-DMA ring
 // The same product with the operands streamed HBM -> LDS by global_load_lds_dwordx4 into an
 // NBUF-deep ring of SP-pixel stages, NBUF-2 stages in flight behind the one being consumed (the
 // register-staged kernel above keeps one stage in flight; at one 8-wave block per CU the HBM
@@ -243,12 +244,26 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wr = wave / WC, wc = wave % WC;
-    const long long s_begin = (long long)blockIdx.x * a.chunk;
+    // (chunk, output block): wider layers (M, K multiples of 256, e.g. 512) split the output in
+    // 256 x KF blocks.  The blocks sharing a chunk take ids 8 apart, i.e. the same XCD (blocks are
+    // dealt to the 8 XCDs round robin), so the second read of each operand slice hits its L2.
+    const int n_ob = (a.M / 256) * a.n_oblk_c;
+    int chunk_id, ob;
+    if (n_ob > 1 && a.n_chunks % 8 == 0) {
+        const int grp = blockIdx.x / (8 * n_ob), rem = blockIdx.x % (8 * n_ob);
+        chunk_id = grp * 8 + rem % 8;
+        ob = rem / 8;
+    } else {
+        chunk_id = blockIdx.x % a.n_chunks;
+        ob = blockIdx.x / a.n_chunks;
+    }
+    const int m0 = (ob / a.n_oblk_c) * 256, k0 = (ob % a.n_oblk_c) * KF;
+    const long long s_begin = (long long)chunk_id * a.chunk;
     const long long s_end = min(s_begin + a.chunk, a.S);
     const int n_st = s_end > s_begin ? (int)((s_end - s_begin) / SP) : 0;  // host: multiples of SP
-    const bool do_bias = a.bpartial != nullptr;
-    const char* dz = reinterpret_cast<const char*>(a.dz);
-    const char* ft = reinterpret_cast<const char*>(a.feat);
+    const bool do_bias = a.bpartial != nullptr && k0 == 0;
+    const char* dz = reinterpret_cast<const char*>(a.dz) + (size_t)m0 * 2;
+    const char* ft = reinterpret_cast<const char*>(a.feat) + (size_t)k0 * 2;
     const size_t ldzb = (size_t)a.ldz * 2, ldfb = (size_t)a.ldf * 2;
 
     const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
@@ -334,7 +349,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         }
     }
 
-    float* out = a.partial + (size_t)blockIdx.x * a.M * a.K;
+    float* out = a.partial + (size_t)chunk_id * a.M * a.K + (size_t)m0 * a.K + k0;
 #pragma unroll
     for (int i = 0; i < RT; ++i)
 #pragma unroll
@@ -348,7 +363,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         float* bs = reinterpret_cast<float*>(smem);
         bs[threadIdx.x] = bsum;
         __syncthreads();
-        if (threadIdx.x < 256) a.bpartial[(size_t)blockIdx.x * a.M + threadIdx.x] = bs[threadIdx.x] + bs[threadIdx.x + 256];
+        if (threadIdx.x < 256)
+            a.bpartial[(size_t)chunk_id * a.M + m0 + threadIdx.x] = bs[threadIdx.x] + bs[threadIdx.x + 256];
     }
 }
 
@@ -524,7 +540,9 @@ static bool wgrad_dma_enabled() {
 #endif
 
 template <int KF>
-static hipError_t launch_wg_dma(const WgArgs& a, int n_chunks, hipStream_t s) {
+static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
+    a.n_chunks = n_chunks;
+    a.n_oblk_c = a.K / KF;
     constexpr int SP = 32;
     constexpr int NBUF = KF == 256 ? MARF_WG_NBUF_H : MARF_WG_NBUF_0;  // ring depth within 160 KB of LDS
     const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024);
@@ -534,7 +552,7 @@ static hipError_t launch_wg_dma(const WgArgs& a, int n_chunks, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_wgrad_dma<NBUF, SP, KF>), dim3(n_chunks), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((k_wgrad_dma<NBUF, SP, KF>), dim3(n_chunks * (a.M / 256) * a.n_oblk_c), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 
@@ -563,8 +581,9 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
     a.n_oblk_c = nc;
     if (dtype == 1) {
         // LDS-DMA ring: 256-wide dz with a 256-wide (hidden) or 96-wide (layer 0, L = 16) feat
-        const bool dma = M == 256 && ldz == 256 && S % 32 == 0 && chunk % 32 == 0 && wgrad_dma_enabled();
-        if (dma && K == 256 && ldf == 256) return launch_wg_dma<256>(a, n_chunks, s);
+        const bool dma = M % 256 == 0 && ldz % 8 == 0 && ldz >= M && S % 32 == 0 && chunk % 32 == 0 &&
+                         (long long)n_chunks * (M / 256) * ((K + 255) / 256) <= 0x7fffffff && wgrad_dma_enabled();
+        if (dma && K % 256 == 0 && ldf % 8 == 0 && ldf >= K) return launch_wg_dma<256>(a, n_chunks, s);
         if (dma && K == 96 && ldf == 96) return launch_wg_dma<96>(a, n_chunks, s);
         if (cfg == 0) return launch_wg<PrecBF16, 2, 4>(a, n_chunks, nr * nc, s);
         if (cfg == 3) return launch_wg<PrecBF16, 2, 2>(a, n_chunks, nr * nc, s);

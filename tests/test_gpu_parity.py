@@ -490,6 +490,42 @@ def test_fused_step_c3_linearity_and_determinism(tmp_path):
         assert torch.equal(a, b), (i, (a - b).abs().max().item())
 
 
+def test_wgrad_dma_wide_layers_bitwise(tmp_path):
+    """512-wide hidden layers (C5 shape): the LDS-DMA weight-gradient kernel splits each output in
+    256 x 256 blocks (and layer 0 in 256 x 96 blocks); its gradients equal the register-staged
+    kernel's bit for bit."""
+    from model import planar
+    from util import EasyDict as edict
+    B = 2
+    opt = make_opt(tmp_path, H=512, W=512, patch_H=256, patch_W=256, batch_size=B, precision="bf16",
+                   arch={"layers": [None, 512, 512, 512, 3], "skip": [], "posenc": {"L_2D": 16}})
+    torch.manual_seed(1)
+    graph = planar.Graph(opt).to(DEV)
+    graph.neural_image.progress.data.fill_(0.3)
+    rng = np.random.default_rng(4)
+    gt = t(rng.random((B, 3, 256, 256)).astype(np.float32))
+    mask = t((rng.random((B, 1, 256, 256)) < 0.85).astype(np.float32))
+    var = edict(images=edict(rgb=gt, masks=mask, masks_eroded=mask, edges=None))
+    graph.need_edges = False
+
+    def run():
+        for p in graph.parameters():
+            p.grad = None
+        v = graph.forward(var)
+        graph.compute_loss(v).rgb.backward()
+        return [p.grad.clone() for p in graph.neural_image.mlp.parameters()]
+
+    g1 = run()
+    os.environ["MARF_WGRAD_DMA"] = "0"
+    try:
+        g2 = run()
+    finally:
+        del os.environ["MARF_WGRAD_DMA"]
+    for i, (a, b) in enumerate(zip(g1, g2)):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b), (i, (a - b).abs().max().item())
+
+
 def test_bf16_gradients_vs_fp32_c3_width(tmp_path):
     """C3 widths (L=16, 4 x 256 hidden: the LDS-DMA hidden-layer weight-gradient kernel and the
     128-pixel tiles): bf16 MLP gradients against the fp32 path from the same state (cosine >= 0.995 and
