@@ -161,10 +161,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for a one-GPU box (never set by the driver): every rank on cuda:0, gloo
+    if os.environ.get("MARF_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("MARF_BENCH_BACKEND", "nccl")  # "nccl" is RCCL on ROCm
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
 
     import marf_hip
     from model import planar
@@ -227,8 +234,24 @@ def main():
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t)
-    loss_v = float(loss.rgb)
+    loss_v = float(loss.rgb.detach())
     assert np.isfinite(loss_v), "loss is not finite"
+
+    # ---- forward-only render rate (reported beside the step): Graph.forward without
+    #      grad = grid -> warp -> posenc -> MLP -> rgb over the same patches (k_mlp_fwd, no saves)
+    with torch.no_grad():
+        for _ in range(2):
+            graph.forward(var, mode="eval")
+        barrier()
+        t0 = time.perf_counter()
+        n_render = max(5, args.steps // 2)
+        for _ in range(n_render):
+            graph.forward(var, mode="eval")
+        barrier()
+        tr = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+        if world > 1:
+            torch.distributed.all_reduce(tr, op=torch.distributed.ReduceOp.MAX)
+        render_pps = world * px_local * n_render / float(tr)
 
     # ---- roofline of the dominant kernel (HIP-event durations measured above, same stream)
     dims = [2 + 4 * L] + hidden + [3]
@@ -282,7 +305,8 @@ def main():
                    "algorithmic_flops_per_px": F,
                    "step_tflops_per_gpu": value / world * F / 1e12,
                    "step_frac_of_peak": value / world * F / peak,
-                   "loss_rgb_last": loss_v},
+                   "loss_rgb_last": loss_v,
+                   "render_pixels_per_s": render_pps},
         "roofline": roof,
         "kernels": per_kernel,
         "kernel_ms_per_step": step_kernel_ms,
