@@ -75,12 +75,12 @@ def pmc_traffic(cfg, precision, kernel):
         return None
 
 
-def make_opt(cfg, precision, B_total):
+def make_opt(cfg, precision, B_total, c2f=True):
     import options
     from util import EasyDict as edict
     canvas, crop, _, L, hidden = CONFIGS[cfg]
     opt = options.load_options("options/planar.yaml")
-    over = {"model": "planar", "yaml": "planar", "seed": 3, "barf_c2f": [0, 0.4], "batch_size": B_total,
+    over = {"model": "planar", "yaml": "planar", "seed": 3, "barf_c2f": [0, 0.4] if c2f else None, "batch_size": B_total,
             "precision": precision, "use_edges": False, "max_iter": 3000,
             "arch": {"layers": [None] + hidden + [3], "skip": [], "posenc": {"L_2D": L}}}
     if canvas:
@@ -155,6 +155,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=list(CONFIGS))
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c2f", action="store_true", help="barf_c2f None (BASELINE config 5: c2f on vs off)")
     ap.add_argument("--cpu-sample-patches", type=int, default=2)
     args = ap.parse_args()
 
@@ -179,7 +180,7 @@ def main():
 
     canvas, crop, per_gpu, L, hidden = CONFIGS[args.config]
     B_total = per_gpu * world
-    opt = make_opt(args.config, args.precision, B_total)
+    opt = make_opt(args.config, args.precision, B_total, c2f=not args.no_c2f)
     opt.device = str(dev)
     h, w = opt.patch_H, opt.patch_W
     torch.manual_seed(opt.seed)
@@ -299,7 +300,8 @@ def main():
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
         "config": {"workload": f"{args.config}: {per_gpu} patches x {h}x{w} px per GPU, L={L}, MLP "
-                               f"{'-'.join(map(str, dims))}, {args.precision}, c2f [0,0.4] at progress 0.2",
+                               f"{'-'.join(map(str, dims))}, {args.precision}, "
+                               + ("c2f off" if args.no_c2f else "c2f [0,0.4] at progress 0.2"),
                    "patches_per_gpu": per_gpu, "pixels_per_step_per_gpu": px_local,
                    "pixels_per_s_per_gpu": value / world, "parallelism": f"dp{world} (patches)",
                    "algorithmic_flops_per_px": F,
