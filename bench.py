@@ -142,7 +142,15 @@ def cpu_baseline(cfg, sample_patches):
         st.step()
         times.append(time.time() - t0)
     px = sample_patches * ch * cw
-    return {"value": px / float(np.mean(times)), "unit": "pixels/s", "cores": int(cores), "kind": "port",
+    cpu = "unknown CPU"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": px / float(np.mean(times)), "unit": "pixels/s", "cores": int(cores), "kind": "port", "cpu": cpu,
             "sample": f"{sample_patches} patches x {ch}x{cw} px, {len(times)} timed oracle steps "
                       f"(numpy fp32 sgemm + C prologue), mean {np.mean(times):.2f} s/step"}
 
