@@ -173,9 +173,12 @@ MARF_DEV void warp_point(const float* Hm, float x, float y, float& u, float& v, 
 }
 
 // Pixel slot -> (x, y) grid point and warped (u, v).  Returns false for padding slots.
+// GRID_ONLY: the caller only runs on the crop grid (the fused step); no coordinate-load branch, so
+// no outstanding-load merge that would make the compiler wait vmcnt(0) here.
+template <bool GRID_ONLY = false>
 MARF_DEV bool slot_point(const GeoDev& g, int b, int p, float& x, float& y, float& u, float& v, float* X) {
     if (p >= g.Np) return false;
-    if (g.mode == 1) {
+    if (!GRID_ONLY && g.mode == 1) {
         u = g.coords[2 * (size_t)p];
         v = g.coords[2 * (size_t)p + 1];
         x = u;

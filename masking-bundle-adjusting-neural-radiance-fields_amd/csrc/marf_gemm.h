@@ -313,7 +313,7 @@ MARF_DEV void c2f_weights_lds(const C2fDev& c2f, int L, float* wsh) {
 // (warp.py:33-81, model/planar.py:451-471; feature layout [u, v, sin_k(u), cos_k(u), sin_k(v),
 // cos_k(v)], zero padded to Kp0).  NPART = 256 / TP threads share a pixel: half of them take u,
 // half v, each a contiguous run of bands, written as bf16 pairs (one 4-byte LDS store per pair).
-template <class P, int TP>
+template <class P, int TP, bool GRID_ONLY = false>
 MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh,
                             typename P::T* act, int lda, int b, int p0) {
     typedef typename P::T T;
@@ -321,7 +321,7 @@ MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, co
     const int L = net.L;
     const int i = threadIdx.x % TP, part = threadIdx.x / TP;
     float x, y, u = 0.f, v = 0.f, X[3];
-    slot_point(geo, b, p0 + i, x, y, u, v, X);
+    slot_point<GRID_ONLY>(geo, b, p0 + i, x, y, u, v, X);
     T* row = act + (size_t)i * lda;
     auto put2 = [&](int col, float a0, float a1) {  // col even
         if constexpr (sizeof(T) == 2) {
@@ -478,7 +478,7 @@ MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
 // (model/planar.py:451-471, warp.py:74-78 backward): per slot d(u, v), then for the grid geometry
 // d(Hx) and one dH[3x3] partial per tile (fixed-order wave + block sums); for explicit coordinates
 // d coords.  `red` needs 4 * TP * 2 floats, `red9` 4 * 9.  smem = the act tile (reused as fp32).
-template <class P, int TP>
+template <class P, int TP, bool GRID_ONLY = false>
 MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh, char* smem, int lda,
                            int wave, int lane, int b, int p0, float* red, float* red9, float* dH_partial,
                            float* d_coords, TileStore<typename P::T>& st, unsigned long long* sp = nullptr) {
@@ -512,7 +512,7 @@ MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, con
     constexpr int NPART = 256 / TP;
     const int i = threadIdx.x % TP, part = threadIdx.x / TP;
     float x, y, u = 0.f, v = 0.f, X[3] = {0.f, 0.f, 1.f};
-    const bool valid = slot_point(geo, b, p0 + i, x, y, u, v, X);
+    const bool valid = slot_point<GRID_ONLY>(geo, b, p0 + i, x, y, u, v, X);
     const float* row = df + (size_t)i * ldf;
     float du = 0.f, dv = 0.f;
     if (part == 0) {

@@ -67,19 +67,26 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
 #endif
 
     STAMP(0);
-    // target + mask of the tile's slots: loaded now, parked in gl until the loss needs them
-    float4 tg = make_float4(0.f, 0.f, 0.f, 0.f);
-    if ((int)threadIdx.x < TP && p0 + (int)threadIdx.x < Np) {
-        const int p = p0 + threadIdx.x;
-        tg.x = a.gt[((size_t)b * 3 + 0) * Np + p];
-        tg.y = a.gt[((size_t)b * 3 + 1) * Np + p];
-        tg.z = a.gt[((size_t)b * 3 + 2) * Np + p];
-        tg.w = a.mask ? a.mask[(size_t)b * Np + p] : 1.0f;
+    // the band weights first: vmcnt retires loads in issue order, so the barrier below must not
+    // wait behind the tile's HBM target loads (those stay in flight through the prologue)
+    const float cw = (int)threadIdx.x < net.L ? a.c2f_w[threadIdx.x] : 0.f;
+    // target + mask of the tile's slots: loaded now, parked in gl until the loss needs them.
+    // Straight-line (every thread loads, padding slots a clamped valid pixel, zeroed after) so the
+    // compiler counts them and the barrier below waits for the band weights only.
+    float4 tg;
+    {
+        const int ti = threadIdx.x & (TP - 1);
+        const int pc = min(p0 + ti, Np - 1);
+        const float* gb = a.gt + (size_t)b * 3 * Np + pc;
+        const float* mb = a.mask ? a.mask + (size_t)b * Np + pc : gb;
+        tg = make_float4(gb[0], gb[Np], gb[2 * (size_t)Np], mb[0]);
+        if (!a.mask) tg.w = 1.0f;
+        if (p0 + ti >= Np) tg = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if ((int)threadIdx.x < net.L) wsh[threadIdx.x] = a.c2f_w[threadIdx.x];
+    if ((int)threadIdx.x < net.L) wsh[threadIdx.x] = cw;
     __syncthreads();
     STAMP(19);
-    tile_prologue<P, TP>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0);
+    tile_prologue<P, TP, true>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0);
     if ((int)threadIdx.x < TP) *reinterpret_cast<float4*>(&gl[threadIdx.x][0]) = tg;
     __syncthreads();
     STAMP(1);
@@ -288,9 +295,9 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
 
     // ---- layer-0 dgrad + posenc / warp adjoint -> dH partial
 #ifdef MARF_STAMPS
-    warp_adjoint<P, TP>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st, sp);
+    warp_adjoint<P, TP, true>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st, sp);
 #else
-    warp_adjoint<P, TP>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st);
+    warp_adjoint<P, TP, true>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st);
 #endif
     STAMP(15);
 }
