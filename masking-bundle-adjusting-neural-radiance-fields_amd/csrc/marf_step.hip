@@ -40,7 +40,12 @@ MARF_DEV i16x4 tr_read16(const u16* p) {
 #define SAVE_DST(ptr, cols) (ptr)
 #endif
 
-template <class P, int TP>
+// BL: every forward bias staged in LDS at the start (sum of the hidden widths <= MARF_STEP_NBIAS):
+// a GEMM's accumulator init reads LDS instead of loading from global behind the previous GEMM's
+// stores (vmcnt retires in issue order), and no bias registers are live across the prologue.
+constexpr int MARF_STEP_NBIAS = 1024;
+
+template <class P, int TP, bool BL>
 __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     typedef typename P::T T;
     constexpr int PT = TP / 32;
@@ -53,6 +58,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     __shared__ __attribute__((aligned(16))) float gl[TP][4];  // sigmoid' gradient per slot (fp32)
     __shared__ __attribute__((aligned(16))) T gT[8][TP];      // the same, channel-major, split hi / lo
     __shared__ float lsum[2][TP];                              // per-slot ((p-g) m)^2 and m
+    __shared__ __attribute__((aligned(16))) float bsh[BL ? MARF_STEP_NBIAS : 4];  // forward biases
 
     const NetDev& net = a.net;
     const int lda = a.lda;
@@ -70,6 +76,10 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     // the band weights first: vmcnt retires loads in issue order, so the barrier below must not
     // wait behind the tile's HBM target loads (those stay in flight through the prologue)
     const float cw = (int)threadIdx.x < net.L ? a.c2f_w[threadIdx.x] : 0.f;
+    if constexpr (BL) {
+        for (int l = 0, off = 0; l < nl - 1; off += net.Mp[l], ++l)
+            for (int e = threadIdx.x; e < net.Mp[l]; e += 256) bsh[off + e] = net.bias[l][e];
+    }
     // target + mask of the tile's slots: loaded now, parked in gl until the loss needs them.
     // Straight-line (every thread loads, padding slots a clamped valid pixel, zeroed after) so the
     // compiler counts them and the barrier below waits for the band weights only.
@@ -97,10 +107,16 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
 
     // ---- hidden layers (forward); the last one is peeled so the last layer's weight fragments
     //      can be in flight behind its epilogue without pinning registers through the loop
+    int boff = 0;  // offset of layer l's bias in bsh
+    auto bias_of = [&](int l) -> const float* {
+        if constexpr (BL) return bsh + boff;
+        else return net.bias[l];
+    };
     auto hidden = [&](int l) {
         const int K = net.Kp[l], M = net.Mp[l], n_rt = M / 32;
         f32x16 acc[RT][PT];
-        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l], st);
+        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, bias_of(l), st);
+        boff += M;
         __syncthreads();  // every wave has consumed the layer input
         STAMP(2 + 2 * l);
         relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x);
@@ -117,7 +133,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         const int l = nl - 2;
         const int K = net.Kp[l], M = net.Mp[l], n_rt = M / 32;
         f32x16 acc[RT][PT];
-        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l], st);
+        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, bias_of(l), st);
         __syncthreads();
         STAMP(2 + 2 * l);
         const T* W = reinterpret_cast<const T*>(net.Wf[nl - 1]);
@@ -340,21 +356,29 @@ __global__ __launch_bounds__(256) void k_loss_final(const double* __restrict__ p
 
 using namespace marf;
 
-template <class P, int TP>
+template <class P, int TP, bool BL>
 static hipError_t launch_step_t(const StepArgs& a, size_t lds, int n_tiles, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_mlp_step<P, TP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipError_t e = hipFuncSetAttribute((const void*)k_mlp_step<P, TP, BL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_mlp_step<P, TP>), dim3(n_tiles), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_mlp_step<P, TP, BL>), dim3(n_tiles), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
+template <class P, int TP>
+static hipError_t launch_step_b(const StepArgs& a, size_t lds, int n_tiles, hipStream_t s) {
+    int nb = 0;
+    for (int l = 0; l + 1 < a.net.n_layers; ++l) nb += a.net.Mp[l];
+    if (nb <= MARF_STEP_NBIAS) return launch_step_t<P, TP, true>(a, lds, n_tiles, s);
+    return launch_step_t<P, TP, false>(a, lds, n_tiles, s);
+}
+
 hipError_t marf_launch_mlp_step(const StepArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s) {
-    if (dtype == 1) return TP == 128 ? launch_step_t<PrecBF16, 128>(a, lds, n_tiles, s) : launch_step_t<PrecBF16, 64>(a, lds, n_tiles, s);
-    return TP == 128 ? launch_step_t<PrecF32, 128>(a, lds, n_tiles, s) : launch_step_t<PrecF32, 64>(a, lds, n_tiles, s);
+    if (dtype == 1) return TP == 128 ? launch_step_b<PrecBF16, 128>(a, lds, n_tiles, s) : launch_step_b<PrecBF16, 64>(a, lds, n_tiles, s);
+    return TP == 128 ? launch_step_b<PrecF32, 128>(a, lds, n_tiles, s) : launch_step_b<PrecF32, 64>(a, lds, n_tiles, s);
 }
 
 hipError_t marf_launch_c2f_weights(const C2fDev& c, int L, float* out, hipStream_t s) {
