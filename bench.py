@@ -164,6 +164,8 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2f", action="store_true", help="barf_c2f None (BASELINE config 5: c2f on vs off)")
+    ap.add_argument("--strong", type=int, default=0, metavar="PATCHES",
+                    help="strong scaling: PATCHES in total split over the ranks (SURVEY §8d: 512)")
     ap.add_argument("--cpu-sample-patches", type=int, default=2)
     args = ap.parse_args()
 
@@ -187,6 +189,10 @@ def main():
     from util import EasyDict as edict
 
     canvas, crop, per_gpu, L, hidden = CONFIGS[args.config]
+    if args.strong:
+        if args.strong % world:
+            raise SystemExit(f"--strong {args.strong} patches do not split over {world} ranks")
+        per_gpu = args.strong // world
     B_total = per_gpu * world
     opt = make_opt(args.config, args.precision, B_total, c2f=not args.no_c2f)
     opt.device = str(dev)
@@ -305,7 +311,7 @@ def main():
     F = flops_per_px(dims)
     out = {
         "metric": METRIC, "value": value, "unit": "pixels/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
         "config": {"workload": f"{args.config}: {per_gpu} patches x {h}x{w} px per GPU, L={L}, MLP "
                                f"{'-'.join(map(str, dims))}, {args.precision}, "
