@@ -307,10 +307,17 @@ class _MLPFunction(torch.autograd.Function):
         shp = coords.shape[:-1]
         c2 = coords.reshape(-1, 2)
         n = c2.shape[0]
-        geo = coords_geometry(c2)
         rgb = torch.empty(n, 3, device=coords.device, dtype=torch.float32)
-        packed = engine.packed_for(params)
         need_grad = any(ctx.needs_input_grad)
+        ctx.empty = n == 0
+        if ctx.empty:
+            # torch's path on an empty batch: an empty [..., 0, 3] prediction and all-zero gradients
+            # (mm over a zero-length axis); nothing to launch.
+            ctx.coord_shape = coords.shape
+            ctx.shapes = [p.shape for p in params]
+            return rgb.view(*shp, 3)
+        geo = coords_geometry(c2)
+        packed = engine.packed_for(params)
         saved = None
         if need_grad:
             saved = torch.empty(max(engine.net.saved_bytes(geo), 1), dtype=torch.uint8, device=coords.device)
@@ -326,6 +333,10 @@ class _MLPFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, d_rgb):
+        if ctx.empty:
+            grads = [torch.zeros(s, device=d_rgb.device, dtype=torch.float32) for s in ctx.shapes]
+            dc = torch.zeros(ctx.coord_shape, device=d_rgb.device, dtype=torch.float32) if ctx.needs_input_grad[0] else None
+            return (dc, None, None, *grads)
         c2, progress, rgb = ctx.saved_tensors
         engine = ctx.engine
         geo = coords_geometry(c2)

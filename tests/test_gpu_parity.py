@@ -298,6 +298,43 @@ def test_coords_forward_backward_vs_oracle(precision, tol, tmp_path):
                                    atol=1e-5 * np.abs(duv).max() + 1e-6)
 
 
+@pytest.mark.parametrize("n", [1, 127, 129, 1000 + 37])
+def test_coords_ragged_counts_vs_oracle(n, tmp_path):
+    """Coordinate counts that leave a partial last pixel tile (128-pixel tiles): fp32 within 1e-5."""
+    from model.planar import NeuralImageFunction
+    opt = make_opt(tmp_path, precision="fp32", arch={"layers": [None, 128, 96, 3], "skip": [], "posenc": {"L_2D": 8}})
+    torch.manual_seed(1)
+    ni = NeuralImageFunction(opt).to(DEV)
+    ni.progress.data.fill_(0.3)
+    coords = np.random.default_rng(n).uniform(-0.6, 0.6, (1, n, 2)).astype(np.float32)
+    c = t(coords).requires_grad_()
+    rgb = ni.forward(c)
+    params = [(l.weight.detach().cpu().numpy(), l.bias.detach().cpu().numpy()) for l in ni.mlp]
+    w = oracle.c2f_weights(np.float32(0.3), [0, 0.4], 8)
+    acts, ref = oracle.mlp_forward(oracle.posenc_features(coords.reshape(-1, 2), 8, w), params)
+    np.testing.assert_allclose(rgb.detach().cpu().numpy().reshape(-1, 3), ref, atol=1e-5)
+    d = np.random.default_rng(n + 1).standard_normal((1, n, 3)).astype(np.float32)
+    rgb.backward(t(d))
+    grads, _ = oracle.mlp_backward(acts, ref, d.reshape(-1, 3), params)
+    for i, l in enumerate(ni.mlp):
+        got, r = l.weight.grad.cpu().numpy(), grads[i][0]
+        assert np.abs(got - r).max() <= 1e-5 * np.abs(r).max() + 1e-7
+
+
+def test_coords_empty_batch(tmp_path):
+    """An empty coordinate batch gives torch's answer: a [B, 0, 3] prediction and zero gradients."""
+    from model.planar import NeuralImageFunction
+    opt = make_opt(tmp_path, precision="fp32", arch={"layers": [None, 128, 96, 3], "skip": [], "posenc": {"L_2D": 8}})
+    ni = NeuralImageFunction(opt).to(DEV)
+    c = torch.zeros(2, 0, 2, device=DEV, requires_grad=True)
+    rgb = ni.forward(c)
+    assert rgb.shape == (2, 0, 3)
+    rgb.sum().backward()
+    assert c.grad.shape == c.shape
+    for l in ni.mlp:
+        assert l.weight.grad is not None and float(l.weight.grad.abs().max()) == 0.0
+
+
 def test_masked_mse_vs_oracle():
     import marf_hip
     rng = np.random.default_rng(1)
