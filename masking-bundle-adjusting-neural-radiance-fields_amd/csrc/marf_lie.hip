@@ -282,13 +282,17 @@ __global__ void k_reduce_dH_lie_bwd(const float* __restrict__ partial, int tiles
         for (int e = 0; e < 9; ++e) acc[e] += (double)p[(size_t)i * 9 + e];
     for (int e = 0; e < 9; ++e) red[t][e] = acc[e];
     __syncthreads();
+    // the nine entries are summed on nine threads at once, each in the fixed order i = 0..63
+    __shared__ float dHs[9];
+    if (t < 9) {
+        double s = 0.0;
+        for (int i = 0; i < 64; ++i) s += red[i][t];
+        dHs[t] = (float)s;
+    }
+    __syncthreads();
     if (t == 0) {
         float dHf[9];
-        for (int e = 0; e < 9; ++e) {
-            double s = 0.0;
-            for (int i = 0; i < 64; ++i) s += red[i][e];
-            dHf[e] = (float)s;
-        }
+        for (int e = 0; e < 9; ++e) dHf[e] = dHs[e];
         // fused step: partials carry the unit-upstream gradient without 1/denominator
         if (gscale)
             for (int e = 0; e < 9; ++e) dHf[e] = dHf[e] * (gscale[0] / denom[0]);

@@ -330,6 +330,9 @@ __global__ __launch_bounds__(256) void k_loss_final(const double* __restrict__ p
                                                     const float* __restrict__ denom_override) {
     __shared__ double rn[256], rm[256];
     double num = 0.0, ms = 0.0;
+    // unrolled so 8 partial loads are in flight per thread (latency-bound single block); the
+    // per-thread summation order is unchanged
+#pragma unroll 8
     for (int i = threadIdx.x; i < n; i += 256) {
         num += part[2 * (size_t)i];
         ms += part[2 * (size_t)i + 1];
