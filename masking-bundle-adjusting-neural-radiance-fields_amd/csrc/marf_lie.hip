@@ -278,7 +278,10 @@ __global__ void k_reduce_dH_lie_bwd(const float* __restrict__ partial, int tiles
     double acc[9];
     for (int e = 0; e < 9; ++e) acc[e] = 0.0;
     const float* p = partial + (size_t)b * tiles_per_patch * 9;
+    // unrolled so the tile partials' loads are in flight together; per-entry order unchanged
+#pragma unroll 8
     for (int i = t; i < tiles_per_patch; i += 64)
+#pragma unroll
         for (int e = 0; e < 9; ++e) acc[e] += (double)p[(size_t)i * 9 + e];
     for (int e = 0; e < 9; ++e) red[t][e] = acc[e];
     __syncthreads();

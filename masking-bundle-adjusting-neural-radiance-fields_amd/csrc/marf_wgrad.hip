@@ -492,6 +492,8 @@ __global__ __launch_bounds__(256) void k_fold_partials(const float* __restrict__
     if (e < E) {
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
         int c = c0;
+        // 2 x 4 loads in flight; acc[u] still sums chunks u, u+4, u+8, ... in order
+#pragma unroll 2
         for (; c + 4 <= c1; c += 4)
 #pragma unroll
             for (int u = 0; u < 4; ++u) acc[u] += partial[(size_t)(c + u) * E + e];
