@@ -38,13 +38,15 @@ extern "C" {
 
 #define MARF_GEO_GRID 0   /* pixels of the centre crop, warped by a per-patch homography */
 #define MARF_GEO_COORDS 1 /* explicit [n][2] coordinates (one point set) */
+#define MARF_GEO_CANVAS 2 /* every pixel of the H x W canvas (use_cropped_images off), warped per patch
+                             (warp.py:54-68 grid; patch_H / patch_W ignored) */
 
 typedef struct marf_net marf_net; /* opaque: MLP shape + padding plan */
 
 typedef struct {
-    int mode;             /* MARF_GEO_GRID or MARF_GEO_COORDS */
-    int B;                /* patches (GRID) ; must be 1 for COORDS */
-    int Np;               /* GRID: patch_H*patch_W (computed); COORDS: number of points */
+    int mode;             /* MARF_GEO_GRID, MARF_GEO_CANVAS or MARF_GEO_COORDS */
+    int B;                /* patches (GRID / CANVAS) ; must be 1 for COORDS */
+    int Np;               /* GRID / CANVAS: computed; COORDS: number of points */
     int H, W;             /* canvas (opt.H, opt.W) */
     int patch_H, patch_W; /* crop (opt.patch_H, opt.patch_W) */
     const float* d_H;     /* GRID: [B][3][3] homographies (from marf_sl3_to_SL3) */

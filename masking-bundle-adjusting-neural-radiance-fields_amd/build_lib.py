@@ -41,15 +41,35 @@ def build(force=False, verbose=True, stamps=False):
 
 
 def _compile(lib_path, extra, verbose):
+    """One hipcc process per translation unit (in parallel), then one link."""
+    import tempfile
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     os.makedirs(os.path.dirname(lib_path), exist_ok=True)
     tmp = lib_path + ".tmp"
-    cmd = [hipcc] + FLAGS + extra + [os.path.join(HERE, "csrc", s) for s in SOURCES] + ["-o", tmp]
     if verbose:
         print("[marf] building", lib_path, flush=True)
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    with tempfile.TemporaryDirectory() as td:
+        objs, procs = [], []
+        cflags = [f for f in FLAGS if f != "-shared"]
+        for src in SOURCES:
+            obj = os.path.join(td, src.replace(".hip", ".o"))
+            objs.append(obj)
+            procs.append(subprocess.Popen([hipcc] + cflags + extra + ["-c", os.path.join(HERE, "csrc", src), "-o", obj],
+                                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+            while sum(p.poll() is None for p in procs) >= jobs:
+                procs[[p.poll() is None for p in procs].index(True)].wait()
+        errs = []
+        for src, p in zip(SOURCES, procs):
+            out = p.communicate()[0]
+            if p.returncode != 0:
+                errs.append(f"{src}:\n{out}")
+        if errs:
+            raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
+        r = subprocess.run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", tmp],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("hipcc link failed:\n" + r.stdout + r.stderr)
     os.replace(tmp, lib_path)
     return lib_path
 

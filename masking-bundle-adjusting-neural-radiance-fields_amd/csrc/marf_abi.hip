@@ -81,8 +81,24 @@ int marf_sl3_to_SL3_backward(const float* d_h, const float* d_dH, float* d_dh, i
 static int make_geo(const marf_geometry* g, GeoDev& d, int TP_pad) {
     if (!g) return fail(MARF_ERR_INVALID, "geometry is NULL");
     memset(&d, 0, sizeof(d));
-    d.mode = g->mode;
-    if (g->mode == MARF_GEO_GRID) {
+    d.mode = g->mode == MARF_GEO_CANVAS ? MARF_GEO_GRID : g->mode;  // the kernels see a window
+    if (g->mode == MARF_GEO_CANVAS) {
+        // warp.py:54-68: every canvas pixel, row-major (no centre-crop integer halving)
+        if (g->B <= 0 || g->H <= 0 || g->W <= 0 || (long long)g->H * g->W > (1LL << 30))
+            return fail(MARF_ERR_INVALID, "canvas geometry: B=%d H=%d W=%d", g->B, g->H, g->W);
+        if (!g->d_H) return fail(MARF_ERR_INVALID, "canvas geometry needs d_H");
+        int mx = std::max(g->H, g->W);
+        d.B = g->B;
+        d.y0 = 0;
+        d.x0 = 0;
+        d.w = g->W;
+        d.Np = g->H * g->W;
+        d.H = g->H;
+        d.W = g->W;
+        d.norm_h = (float)((double)g->H / (double)mx);
+        d.norm_w = (float)((double)g->W / (double)mx);
+        d.Hm = g->d_H;
+    } else if (g->mode == MARF_GEO_GRID) {
         if (g->B <= 0 || g->H <= 0 || g->W <= 0 || g->patch_H <= 1 || g->patch_W <= 1 || g->patch_H > g->H ||
             g->patch_W > g->W)
             return fail(MARF_ERR_INVALID, "grid geometry: B=%d H=%d W=%d patch=%dx%d", g->B, g->H, g->W, g->patch_H,
@@ -521,7 +537,7 @@ static void plan_step(const marf_net* n, long long S, StepPlan& p) {
 
 size_t marf_step_saved_bytes(const marf_net* net, const marf_geometry* geo) {
     GeoDev g;
-    if (!net || !geo || geo->mode != MARF_GEO_GRID || make_geo(geo, g, MARF_TILE_PAD) != MARF_OK) return 0;
+    if (!net || !geo || geo->mode == MARF_GEO_COORDS || make_geo(geo, g, MARF_TILE_PAD) != MARF_OK) return 0;
     StepPlan p;
     plan_step(net, (long long)g.B * g.Np_pad, p);
     return p.total;
@@ -531,7 +547,7 @@ int marf_step_forward(const marf_net* net, const marf_geometry* geo, const marf_
                       const float* d_gt, const float* d_mask, const float* d_denom_override, float* d_rgb,
                       float* d_loss_out, void* d_saved, void* stream) {
     if (!net || !d_packed || !d_gt || !d_loss_out || !d_saved) return fail(MARF_ERR_INVALID, "step_forward: NULL argument");
-    if (!geo || geo->mode != MARF_GEO_GRID) return fail(MARF_ERR_INVALID, "step_forward: needs the grid geometry");
+    if (!geo || geo->mode == MARF_GEO_COORDS) return fail(MARF_ERR_INVALID, "step_forward: needs a pixel-grid geometry");
     hipStream_t s = (hipStream_t)stream;
     StepArgs a;
     memset(&a, 0, sizeof(a));
@@ -575,7 +591,7 @@ int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void
                        int lie_batch, const float* d_gout, const float* d_loss_out, float* d_dparams, float* d_dh,
                        void* stream) {
     if (!net || !d_saved || !d_gout || !d_loss_out) return fail(MARF_ERR_INVALID, "step_backward: NULL argument");
-    if (!geo || geo->mode != MARF_GEO_GRID) return fail(MARF_ERR_INVALID, "step_backward: needs the grid geometry");
+    if (!geo || geo->mode == MARF_GEO_COORDS) return fail(MARF_ERR_INVALID, "step_backward: needs a pixel-grid geometry");
     if (d_dh && !d_h_params) return fail(MARF_ERR_INVALID, "step_backward: d_dh requested without the warp parameters");
     hipStream_t s = (hipStream_t)stream;
     GeoDev g;

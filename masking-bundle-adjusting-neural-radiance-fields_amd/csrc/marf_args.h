@@ -70,6 +70,11 @@ struct PackArgs {
     PackLayer ly[MARF_MAX_LAYERS];
 };
 
+// Raise a kernel's dynamic-LDS limit to at least `lds` bytes before a launch.  The limit set so
+// far is tracked per (device, kernel) under a mutex, so a later launch of the same instantiation
+// with a larger tile (a wider net) raises it again, and concurrent host threads do not race.
+hipError_t ensure_dynamic_lds(const void* kernel, size_t lds);
+
 }  // namespace marf
 
 hipError_t marf_launch_sl3(const float* h, float* H, int B, int batch_hint, hipStream_t s);

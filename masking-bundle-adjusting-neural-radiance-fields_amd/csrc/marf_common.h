@@ -56,7 +56,14 @@ MARF_DEV float bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
 // diagnostic builds: round an fp32-path value to bf16 precision (numerics experiments)
 MARF_DEV float diag_round_bf16(float x) { return bf2f(f2bf(x)); }
 MARF_DEV float diag_round_fp16(float x) { return (float)(_Float16)x; }
-#if defined(MARF_DIAG_ACT_FP16) || defined(MARF_DIAG_FEAT_FP16)
+// a value carried as a bf16 hi + lo pair (~16 significant bits: what split-bf16 GEMMs see)
+MARF_DEV float diag_round_split(float x) {
+    const float h = bf2f(f2bf(x));
+    return h + bf2f(f2bf(x - h));
+}
+#if defined(MARF_DIAG_SPLIT)
+#define DIAG_RND diag_round_split
+#elif defined(MARF_DIAG_ACT_FP16) || defined(MARF_DIAG_FEAT_FP16)
 #define DIAG_RND diag_round_fp16
 #else
 #define DIAG_RND diag_round_bf16

@@ -155,7 +155,7 @@ __global__ void k_pack(const float* __restrict__ params, char* __restrict__ pack
             frag_coord<P>(e, nkf, last16, m, k);
             float wv = m < L.M && k < L.K ? W[(size_t)m * L.K + k] : 0.f;
 #if defined(MARF_DIAG_W_BF16)
-            wv = diag_round_bf16(wv);
+            wv = DIAG_RND(wv);
 #elif defined(MARF_DIAG_W_FP16)
             wv = diag_round_fp16(wv);
 #endif

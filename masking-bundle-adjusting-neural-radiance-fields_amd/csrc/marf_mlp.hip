@@ -172,11 +172,9 @@ using namespace marf;
 
 template <class P, int TP>
 static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, int n_tiles, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_mlp_fwd<P, TP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    {
+        hipError_t e = ensure_dynamic_lds((const void*)k_mlp_fwd<P, TP>, lds);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     hipLaunchKernelGGL((k_mlp_fwd<P, TP>), dim3(n_tiles), dim3(256), lds, s, a);
     return hipGetLastError();
@@ -184,11 +182,9 @@ static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, int n_tiles, hipStr
 
 template <class P, int TP>
 static hipError_t launch_bwd_t(const BwdArgs& a, size_t lds, int n_tiles, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_mlp_bwd<P, TP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    {
+        hipError_t e = ensure_dynamic_lds((const void*)k_mlp_bwd<P, TP>, lds);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     hipLaunchKernelGGL((k_mlp_bwd<P, TP>), dim3(n_tiles), dim3(256), lds, s, a);
     return hipGetLastError();

@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "marf_args.h"
 #include "marf_prof.h"
 
 namespace {
@@ -69,6 +70,24 @@ static void drain() {
     }
     g_pending.clear();
 }
+
+namespace marf {
+
+hipError_t ensure_dynamic_lds(const void* kernel, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, size_t> set_so_far;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(mu);
+    size_t& cur = set_so_far[{dev, kernel}];
+    if (cur >= lds) return hipSuccess;
+    e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e == hipSuccess) cur = lds;
+    return e;
+}
+
+}  // namespace marf
 
 extern "C" {
 

@@ -361,11 +361,9 @@ using namespace marf;
 
 template <class P, int TP, bool BL>
 static hipError_t launch_step_t(const StepArgs& a, size_t lds, int n_tiles, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_mlp_step<P, TP, BL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    {
+        hipError_t e = ensure_dynamic_lds((const void*)k_mlp_step<P, TP, BL>, lds);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     hipLaunchKernelGGL((k_mlp_step<P, TP, BL>), dim3(n_tiles), dim3(256), lds, s, a);
     return hipGetLastError();

@@ -519,11 +519,9 @@ static hipError_t launch_wg(const WgArgs& a, int n_chunks, int n_oblk, hipStream
     constexpr int PADE = sizeof(T) == 2 ? 32 : 4;
     size_t lds = (size_t)SP * (BM + PADE + BN + PADE) * sizeof(T);
     if (lds < 512 * sizeof(float)) lds = 512 * sizeof(float);
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_wgrad<P, RT, CT, SP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    {
+        hipError_t e = ensure_dynamic_lds((const void*)k_wgrad<P, RT, CT, SP>, lds);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     hipLaunchKernelGGL((k_wgrad<P, RT, CT, SP>), dim3(n_chunks, n_oblk), dim3(512), lds, s, a);
     return hipGetLastError();
@@ -548,11 +546,9 @@ static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
     constexpr int SP = 32;
     constexpr int NBUF = KF == 256 ? MARF_WG_NBUF_H : MARF_WG_NBUF_0;  // ring depth within 160 KB of LDS
     const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024);
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_wgrad_dma<NBUF, SP, KF>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    {
+        hipError_t e = ensure_dynamic_lds((const void*)k_wgrad_dma<NBUF, SP, KF>, lds);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     hipLaunchKernelGGL((k_wgrad_dma<NBUF, SP, KF>), dim3(n_chunks * (a.M / 256) * a.n_oblk_c), dim3(512), lds, s, a);
     return hipGetLastError();

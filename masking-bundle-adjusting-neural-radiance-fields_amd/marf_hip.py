@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MARF_LIB") or os.path.join(_HERE, "lib", "libmarf.so")
 
 MARF_FP32, MARF_BF16 = 0, 1
-GEO_GRID, GEO_COORDS = 0, 1
+GEO_GRID, GEO_COORDS, GEO_CANVAS = 0, 1, 2
 
 _c_int, _c_ll, _c_dbl, _c_vp, _c_sz = ctypes.c_int, ctypes.c_longlong, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
 
@@ -249,9 +249,10 @@ class Net:
         return lib().marf_workspace_bytes(self._h, ctypes.byref(geo))
 
 
-def grid_geometry(B, H, W, patch_H, patch_W, Hm=None):
+def grid_geometry(B, H, W, patch_H, patch_W, Hm=None, crop=True):
+    """Centre-crop pixel grid (crop) or every canvas pixel (use_cropped_images off, warp.py:54-68)."""
     g = Geometry()
-    g.mode, g.B, g.H, g.W, g.patch_H, g.patch_W = GEO_GRID, B, H, W, patch_H, patch_W
+    g.mode, g.B, g.H, g.W, g.patch_H, g.patch_W = GEO_GRID if crop else GEO_CANVAS, B, H, W, patch_H, patch_W
     g.d_H = None if Hm is None else Hm.data_ptr()
     return g
 
@@ -302,13 +303,13 @@ class _MLPFunction(torch.autograd.Function):
     """NeuralImageFunction.forward on explicit coordinates (model/planar.py:429-449)."""
 
     @staticmethod
-    def forward(ctx, coords, progress, engine, *params):
+    def forward(ctx, coords, progress, engine, grad_on, *params):
         coords = _f32(coords, "coord_2d")
         shp = coords.shape[:-1]
         c2 = coords.reshape(-1, 2)
         n = c2.shape[0]
         rgb = torch.empty(n, 3, device=coords.device, dtype=torch.float32)
-        need_grad = any(ctx.needs_input_grad)
+        need_grad = grad_on and any(ctx.needs_input_grad)
         ctx.empty = n == 0
         if ctx.empty:
             # torch's path on an empty batch: an empty [..., 0, 3] prediction and all-zero gradients
@@ -336,7 +337,7 @@ class _MLPFunction(torch.autograd.Function):
         if ctx.empty:
             grads = [torch.zeros(s, device=d_rgb.device, dtype=torch.float32) for s in ctx.shapes]
             dc = torch.zeros(ctx.coord_shape, device=d_rgb.device, dtype=torch.float32) if ctx.needs_input_grad[0] else None
-            return (dc, None, None, *grads)
+            return (dc, None, None, None, *grads)
         c2, progress, rgb = ctx.saved_tensors
         engine = ctx.engine
         geo = coords_geometry(c2)
@@ -350,7 +351,7 @@ class _MLPFunction(torch.autograd.Function):
                                    _ptr(dcoords), _stream(c2)))
         grads = _split_grads(dflat, ctx.shapes)
         dc = None if dcoords is None else dcoords.view(ctx.coord_shape)
-        return (dc, None, None, *grads)
+        return (dc, None, None, None, *grads)
 
 
 class _PlanarRenderFunction(torch.autograd.Function):
@@ -376,6 +377,7 @@ class _PlanarRenderFunction(torch.autograd.Function):
                                   _ptr(saved), st))
         ctx.save_for_backward(w, progress, rgb)
         ctx.Hm, ctx.h_local, ctx.saved_buf, ctx.packed, ctx.engine = Hm, h_local, saved, packed, engine
+        ctx.gen = _BUFS.generation("planar_saved", w.device)
         ctx.b0, ctx.b1 = b0, b1
         ctx.shapes = [p.shape for p in params]
         return rgb
@@ -384,6 +386,9 @@ class _PlanarRenderFunction(torch.autograd.Function):
     def backward(ctx, d_rgb):
         w, progress, rgb = ctx.saved_tensors
         engine = ctx.engine
+        if ctx.gen != _BUFS.generation("planar_saved", w.device):
+            raise RuntimeError("libmarf: the render's saved activations were reused by a later forward; "
+                               "call backward() before the next Graph.forward")
         Bl = ctx.b1 - ctx.b0
         geo = engine.grid_geo(Bl, ctx.Hm)
         d_rgb = _f32(d_rgb, "d_rgb")
@@ -488,6 +493,8 @@ def render_step(warp_weight, progress, engine, params, gt, mask, denom_override=
 
 
 def geo_np(engine):
+    if not engine.crop:
+        return engine.H * engine.W
     h = (engine.H // 2 + engine.patch_H // 2) - (engine.H // 2 - engine.patch_H // 2)
     w = (engine.W // 2 + engine.patch_W // 2) - (engine.W // 2 - engine.patch_W // 2)
     return h * w
@@ -496,10 +503,11 @@ def geo_np(engine):
 class Engine:
     """Library-side state of one NeuralImageFunction: net plan, packed weights, c2f, geometry."""
 
-    def __init__(self, dims, L, dtype, c2f, H, W, patch_H, patch_W, lie_batch=0):
+    def __init__(self, dims, L, dtype, c2f, H, W, patch_H, patch_W, lie_batch=0, crop=True):
         self.net = Net(dims, L, dtype)
         self.c2f = c2f
         self.H, self.W, self.patch_H, self.patch_W = H, W, patch_H, patch_W
+        self.crop = bool(crop)
         self._lie_batch = lie_batch
         self._packed = None
         self._packed_version = None
@@ -510,7 +518,7 @@ class Engine:
         return self._lie_batch if self._lie_batch > 0 else B
 
     def grid_geo(self, B, Hm):
-        return grid_geometry(B, self.H, self.W, self.patch_H, self.patch_W, Hm)
+        return grid_geometry(B, self.H, self.W, self.patch_H, self.patch_W, Hm, self.crop)
 
     def packed_for(self, params):
         """Pack the fp32 master weights into the MFMA operand layouts when they changed (tracked by
@@ -548,11 +556,31 @@ def flat_view(tensors):
 
 def render_train(warp_weight, progress, engine, params, b0=0, b1=None):
     b1 = warp_weight.shape[0] if b1 is None else b1
+    if not torch.is_grad_enabled():
+        return render_nograd(warp_weight, progress, engine, params, b0, b1)
     return _PlanarRenderFunction.apply(warp_weight, progress, engine, b0, b1, *params)
 
 
+def render_nograd(warp_weight, progress, engine, params, b0, b1):
+    """Graph.forward without autograd (evaluation / render rate): the same fused grid -> warp ->
+    posenc -> MLP kernel, nothing saved for a backward."""
+    w = _f32(warp_weight, "warp_param")
+    Bl = b1 - b0
+    h_local = w[b0:b1].contiguous()
+    Hm = torch.empty(Bl, 3, 3, device=w.device, dtype=torch.float32)
+    st = _stream(w)
+    _check(lib().marf_sl3_to_SL3(_ptr(h_local), _ptr(Hm), Bl, engine.lie_batch(w.shape[0]), st))
+    geo = engine.grid_geo(Bl, Hm)
+    rgb = torch.empty(Bl, geo_np(engine), 3, device=w.device, dtype=torch.float32)
+    packed = engine.packed_for(params)
+    cf = make_c2f(progress, engine.c2f)
+    _check(lib().marf_forward(engine.net.handle, ctypes.byref(geo), ctypes.byref(cf), _ptr(packed), _ptr(rgb), None,
+                              st))
+    return rgb
+
+
 def mlp_forward(coords, progress, engine, params):
-    return _MLPFunction.apply(coords, progress, engine, *params)
+    return _MLPFunction.apply(coords, progress, engine, torch.is_grad_enabled(), *params)
 
 
 # ====================================================================== loss

@@ -138,7 +138,8 @@ class Model(torch.nn.Module):
         var.images = self.images
         var = util.move_to_device(var, self.opt.device)
         loader = tqdm.trange(self.opt.max_iter, desc="Training", leave=False, disable=self.rank != 0)
-        var = self.graph.forward(var)
+        with torch.no_grad():  # the frame-0 render only (visualize re-renders the canvas)
+            var = self.graph.forward(var)
         self.visualize(var, step=0)
         for _ in loader:
             self.train_iteration(var, loader)
@@ -182,7 +183,7 @@ class Model(torch.nn.Module):
 
     def train_iteration(self, var, loader):
         """One optimisation step in the reference's order (model/planar.py:187-209)."""
-        self.timer.it_start = time.time()
+        t_start = time.time()
         log_now = (self.it + 1) % self.opt.freq.scalar == 0
         self.graph.need_edges = bool(self.opt.use_edges and log_now)
         self.optim.zero_grad()
@@ -201,8 +202,8 @@ class Model(torch.nn.Module):
         self.it += 1
         if log_now:
             loader.set_postfix(it=self.it, loss=f"{float(loss.all):.3f}")
-        self.timer.it_end = time.time()
-        util.update_timer(self.opt, self.timer, self.ep, len(loader))
+        self.timer.it = time.time() - t_start
+        self.timer.it_mean = self.timer.it if self.timer.it_mean is None else 0.99 * self.timer.it_mean + 0.01 * self.timer.it
         self.graph.neural_image.progress.data.fill_(self.it / self.opt.max_iter)
         return loss
 
@@ -291,6 +292,7 @@ class Graph(torch.nn.Module):
             raise AssertionError("only the 8-dof sl(3) homography warp exists (warp.py:72-80)")
         self.shard = None
         self.loss_denominator = None
+        self.edge_denominator = None
         self.need_edges = True
 
     def set_shard(self, rank, world, images):
@@ -306,6 +308,9 @@ class Graph(torch.nn.Module):
         else:
             d = torch.tensor([3.0 * B * self.h * self.w], device=self.opt.device)
         self.loss_denominator = d  # global (all patches are loaded on every rank)
+        me = images.get("masks_eroded") if images is not None else None
+        # the (logging-only) edge term's denominator 3*sum(masks_eroded), global as well
+        self.edge_denominator = None if me is None else (me.sum().to(torch.float64) * 3).to(self.opt.device)
 
     def _range(self):
         return self.shard if self.shard is not None else (0, self.batch_size)
@@ -319,7 +324,7 @@ class Graph(torch.nn.Module):
             # training forward: the target is known, so the loss and the whole backward are
             # computed in the same pass (marf_step_forward); compute_loss picks the loss up
             masks = imgs.masks[b0:b1] if imgs.get("masks") is not None else None
-            denom = self.loss_denominator if (self.shard is not None and masks is not None) else None
+            denom = self.loss_denominator if self.shard is not None else None
             rgb, loss_rgb = self.neural_image.render_step(self.warp_param.weight, imgs.rgb[b0:b1], masks, denom, b0, b1)
             var.fused_loss = (loss_rgb, imgs.rgb, imgs.get("masks"))
         else:
@@ -348,7 +353,12 @@ class Graph(torch.nn.Module):
             if self.opt.use_edges:
                 if var.get("edge_prediction") is not None and imgs.get("edges") is not None:
                     me = imgs.masks_eroded[b0:b1] if imgs.get("masks_eroded") is not None else None
-                    edge_loss = self.mse_loss(var.edge_prediction, imgs.edges[b0:b1], me)
+                    if self.shard is not None and me is not None and self.edge_denominator is not None:
+                        # this rank's share of the global masked MSE: the per-rank terms sum to it
+                        diff = (var.edge_prediction - imgs.edges[b0:b1]) * me
+                        edge_loss = (diff ** 2).sum() / self.edge_denominator
+                    else:
+                        edge_loss = self.mse_loss(var.edge_prediction, imgs.edges[b0:b1], me)
                 else:  # edges are evaluated at logging steps only (they carry no gradient)
                     edge_loss = torch.zeros((), dtype=torch.float64, device=rgb_loss.device)
             else:
@@ -370,7 +380,7 @@ class Graph(torch.nn.Module):
             pred_bn3 = pred.permute(0, 2, 3, 1).reshape(B, -1, 3)
             gt = labels.reshape(B, 3, -1)
             m = None if masks is None else masks.reshape(B, 1, -1)
-            denom = self.loss_denominator if (self.shard is not None and masks is not None) else None
+            denom = self.loss_denominator if self.shard is not None else None
             return marf_hip.masked_mse(pred_bn3, gt, m, denom)
         diff = pred.contiguous() - labels
         if masks is None:
@@ -436,7 +446,7 @@ class NeuralImageFunction(torch.nn.Module):
             dims = [self.input_dim] + [int(d) for d in list(o.arch.layers)[1:]]
             ph, pw = (o.patch_H, o.patch_W) if o.use_cropped_images else (o.H, o.W)
             e = marf_hip.Engine(dims, self.L, _precision(o), list(o.barf_c2f) if o.barf_c2f else None,
-                                o.H, o.W, ph, pw, lie_batch=int(o.batch_size))
+                                o.H, o.W, ph, pw, lie_batch=int(o.batch_size), crop=bool(o.use_cropped_images))
             self._engines[key] = e
         return e
 

@@ -19,7 +19,7 @@ import torch
 import yaml
 
 from util import EasyDict as edict
-from util import log, to_dict
+from util import log, plain_dict
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -108,9 +108,9 @@ def save_options_file(opt):
     if os.path.isfile(fname):
         with open(fname) as f:
             old = yaml.safe_load(f)
-        if old != to_dict(opt):
+        if old != plain_dict(opt):
             print("existing options file differs; overwriting")
         else:
             print("existing options file found (identical)")
     with open(fname, "w") as f:
-        yaml.safe_dump(to_dict(opt), f, default_flow_style=False, indent=4)
+        yaml.safe_dump(plain_dict(opt), f, default_flow_style=False, indent=4)

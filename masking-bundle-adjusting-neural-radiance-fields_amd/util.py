@@ -1,7 +1,6 @@
-"""Small host utilities with the reference's names (util.py:44-115): console log, timer,
-device moves, layer dims.  No termcolor / ipdb dependency."""
-import time
-
+"""Host helpers the planar engine needs (the reference keeps its equivalents in util.py:44-115):
+an attribute dict for options, a plain console logger, a device mover for the `var` bundle, the
+layer-width pairing of define_network and the hex colour parser used for the patch boxes."""
 import torch
 
 
@@ -41,7 +40,7 @@ edict = EasyDict
 
 
 class Log:
-    """Console logger (util.py:44-67)."""
+    """Console logger with the reference's method names (no colour codes)."""
 
     def process(self, pid):
         print(f"Process ID: {pid}")
@@ -53,57 +52,47 @@ class Log:
         print(message)
 
     def options(self, opt, level=0):
-        for key, value in sorted(opt.items()):
+        pad = "   " * level
+        for key in sorted(opt):
+            value = opt[key]
             if isinstance(value, dict):
-                print("   " * level + "* " + key + ":")
+                print(f"{pad}* {key}:")
                 self.options(value, level + 1)
             else:
-                print("   " * level + "* " + key + ":", value)
+                print(f"{pad}* {key}: {value}")
 
 
 log = Log()
 
 
-def update_timer(opt, timer, ep, it_per_ep):
-    """Moving-average iteration timer (util.py:69-79)."""
-    if not opt.max_epoch:
-        return
-    momentum = 0.99
-    timer.elapsed = time.time() - timer.start
-    timer.it = timer.it_end - timer.it_start
-    timer.it_mean = timer.it_mean * momentum + timer.it * (1 - momentum) if timer.it_mean is not None else timer.it
-    timer.arrival = timer.it_mean * it_per_ep * (opt.max_epoch - ep)
-
-
 def move_to_device(x, device):
-    """util.py:81-95."""
-    if isinstance(x, dict):
-        for k, v in x.items():
-            x[k] = move_to_device(v, device)
-    elif isinstance(x, list):
-        for i, e in enumerate(x):
-            x[i] = move_to_device(e, device)
-    elif isinstance(x, tuple) and hasattr(x, "_fields"):
-        return type(x)(**move_to_device(x._asdict(), device))
-    elif isinstance(x, torch.Tensor):
+    """Recursively move every tensor inside dicts / lists / namedtuples to `device` (dicts and
+    lists in place, as the engine's `var` bundle expects)."""
+    if torch.is_tensor(x):
         return x.to(device=device)
+    if isinstance(x, dict):
+        for key in list(x.keys()):
+            x[key] = move_to_device(x[key], device)
+        return x
+    if isinstance(x, list):
+        x[:] = [move_to_device(e, device) for e in x]
+        return x
+    if isinstance(x, tuple) and hasattr(x, "_fields"):
+        return type(x)(*(move_to_device(e, device) for e in x))
     return x
 
 
-def to_dict(d, dict_type=dict):
-    d = dict_type(d)
-    for k, v in d.items():
-        if isinstance(v, dict):
-            d[k] = to_dict(v, dict_type)
-    return d
+def plain_dict(d):
+    """Nested attribute dicts -> plain dicts (what yaml.safe_dump accepts)."""
+    return {k: plain_dict(v) if isinstance(v, dict) else v for k, v in d.items()}
 
 
-def get_layer_dims(layers):
-    """[(k_in, k_out), ...] from a layer-width list (util.py:105-108)."""
-    return list(zip(layers[:-1], layers[1:]))
+def get_layer_dims(widths):
+    """Consecutive width pairs [(k_in, k_out), ...] of an MLP width list."""
+    return [(widths[i], widths[i + 1]) for i in range(len(widths) - 1)]
 
 
 def colorcode_to_number(code):
-    ords = [ord(c) for c in code[1:]]
-    ords = [n - 48 if n < 58 else n - 87 for n in ords]
-    return (ords[0] * 16 + ords[1], ords[2] * 16 + ords[3], ords[4] * 16 + ords[5])
+    """'#RRGGBB' -> (r, g, b) integers."""
+    h = code.lstrip("#")
+    return tuple(int(h[i:i + 2], 16) for i in (0, 2, 4))

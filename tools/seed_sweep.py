@@ -35,10 +35,11 @@ def main():
             with tempfile.TemporaryDirectory() as d:
                 psnr, w = T._run_c1(prec, d, iters=a.iters, seed=s)
             r = dict(precision=prec, seed=s, psnr=float(psnr[-1]), psnr_mean10=float(np.mean(psnr[-10:])),
-                     warps=w.tolist(), secs=round(time.time() - t0, 1))
+                     warps=w.tolist(), secs=round(time.time() - t0, 1), lib=os.environ.get("MARF_LIB", "default"),
+                     warp_err=float(np.abs(w[1:] - T.REF_WARPS_3000).max()), psnr_traj=[float(x) for x in psnr])
             res.append(r)
             print(f"{prec:5s} seed {s}: final PSNR {r['psnr']:.3f} dB (mean of last 10 logged {r['psnr_mean10']:.3f}) "
-                  f"in {r['secs']} s", flush=True)
+                  f"max |warp - ref| {r['warp_err']:.3e} in {r['secs']} s [{r['lib']}]", flush=True)
             os.makedirs(os.path.dirname(a.out), exist_ok=True)
             json.dump(res, open(a.out, "w"))
     for prec in a.precisions:
