@@ -161,7 +161,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=list(CONFIGS))
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16x3", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2f", action="store_true", help="barf_c2f None (BASELINE config 5: c2f on vs off)")
     ap.add_argument("--strong", type=int, default=0, metavar="PATCHES",
@@ -281,11 +281,11 @@ def main():
         "wgrad_hidden": S * 2 * hidden[0] * hidden[0],
         "wgrad_l0": S * 2 * dims[0] * dims[1],
     }
-    kbytes = step_kernel_bytes(S, Kp0, hidden, 2 if args.precision == "bf16" else 4)
+    kbytes = step_kernel_bytes(S, Kp0, hidden, 4 if args.precision == "fp32" else 2)
     per_kernel = {k: {"avg_ms": v[0] / v[1], "launches_per_step": v[1] / args.steps} for k, v in prof.items()}
     step_kernel_ms = sum(v[0] for v in prof.values()) / args.steps
     dom = max(prof.items(), key=lambda kv: kv[1][0])[0] if prof else None
-    peak = PEAK_BF16 if args.precision == "bf16" else PEAK_FP32
+    peak = PEAK_FP32 if args.precision == "fp32" else PEAK_BF16
     roof = None
     if dom in kflops:
         avg_s = prof[dom][0] / prof[dom][1] / 1e3

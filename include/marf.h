@@ -35,6 +35,8 @@ extern "C" {
 
 #define MARF_FP32 0
 #define MARF_BF16 1
+#define MARF_BF16X3 2 /* split bf16: weights and forward activations as bf16 hi + lo pairs (hi*hi + hi*lo + lo*hi
+                         forward, hi + lo weights in the dgrad), bf16 dz / saved tensors; fused step only */
 
 #define MARF_GEO_GRID 0   /* pixels of the centre crop, warped by a per-patch homography */
 #define MARF_GEO_COORDS 1 /* explicit [n][2] coordinates (one point set) */

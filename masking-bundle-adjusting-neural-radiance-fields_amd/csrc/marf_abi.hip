@@ -42,8 +42,18 @@ static int check_hip(hipError_t e, const char* what) {
 
 static inline long long rup(long long x, long long m) { return (x + m - 1) / m * m; }
 
+// step2 plan (the pixel-per-wave fused step, marf_step2.hip), filled by plan_step2_net
+struct Step2NetPlan {
+    int variant;           // -1: not available for this net; 0: bf16 (8 waves); 1: split bf16 (4 waves)
+    int NW, HM, MAXR, NMW, slot, nk0, nta, n_stages, nbias, Kl, ldf0;
+    int nrt[MARF_MAX_LAYERS], nrtb[MARF_MAX_LAYERS], boff[MARF_MAX_LAYERS];
+    size_t prog_off, bias_off, kmap_off, end_off;
+};
+
 struct marf_net {
     int n_layers, L, D, dtype;
+    int kdt;  // kernel arithmetic of the generic kernels: 0 fp32, 1 bf16 (MARF_BF16 and MARF_BF16X3)
+    Step2NetPlan s2;
     int dims[MARF_MAX_LAYERS + 1];
     int Kp[MARF_MAX_LAYERS], Mp[MARF_MAX_LAYERS], Mt[MARF_MAX_LAYERS];
     long long w_off[MARF_MAX_LAYERS], b_off[MARF_MAX_LAYERS], param_count;
@@ -53,6 +63,54 @@ struct marf_net {
     size_t lds_fwd, lds_bwd, lds_step;
     int elem;  // bytes per stored element
 };
+
+static bool step2_env_enabled() {
+    const char* e = getenv("MARF_STEP2");  // plain bf16 on the pixel-per-wave kernel: opt-in ("1")
+    return e && e[0] == '1';
+}
+
+// Which pixel-per-wave variant (marf_step2.hip) runs this net, its weight-program shape and the
+// byte layout of the program / bias table / layer-0 column map appended to the packed buffer.
+static void plan_step2_net(marf_net* n) {
+    Step2NetPlan& q = n->s2;
+    memset(&q, 0, sizeof(q));
+    q.variant = -1;
+    const int nl = n->n_layers;
+    if (n->kdt != 1 || nl < 2 || nl > 5 || n->L > 32) return;
+    for (int l = 0; l < nl - 1; ++l)
+        if (n->Mp[l] > 256) return;
+    q.HM = 256;
+    q.variant = n->dtype == MARF_BF16X3 ? 1 : 0;
+    {
+        const char* e = getenv("MARF_STEP2_NW4");  // diagnostic: plain bf16 on 4 waves per block
+        if (q.variant == 0 && e && e[0] == '1') q.variant = 2;
+    }
+    q.NW = q.variant == 0 ? 8 : 4;
+    q.MAXR = 4;
+    q.NMW = q.HM / 64;
+    q.slot = (q.HM / 16) * 1024 * (q.variant == 1 ? 2 : 1);
+    q.nk0 = (n->L + 3) / 4 + 1;
+    q.nta = (2 * n->L + 1 + 15) / 16;
+    q.ldf0 = (int)rup(16 * q.nk0, 32);
+    q.Kl = n->Kp[nl - 1];
+    int st = 0, bo = 0;
+    for (int l = 0; l < nl; ++l) {
+        q.nrt[l] = l == nl - 1 ? 1 : n->Mp[l] / 32;
+        q.nrtb[l] = l == 0 ? q.nta : n->Kp[l] / 32;
+        q.boff[l] = bo;
+        bo += l == nl - 1 ? 32 : n->Mp[l];
+    }
+    q.nbias = bo;
+    for (int l = 0; l < nl - 1; ++l) st += q.nrt[l];
+    st += 1 + q.nrtb[nl - 1];
+    for (int l = nl - 2; l >= 1; --l) st += q.nrtb[l];
+    st += q.nta;
+    q.n_stages = st;
+    q.prog_off = rup((long long)n->packed_bytes, 4096);
+    q.bias_off = q.prog_off + (size_t)st * q.slot;
+    q.kmap_off = rup((long long)(q.bias_off + (size_t)q.nbias * 4), 256);
+    q.end_off = rup((long long)(q.kmap_off + (size_t)n->D * 4), 256);
+}
 
 extern "C" {
 
@@ -191,7 +249,8 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
     *out = nullptr;
     if (n_layers < 2 || n_layers > MARF_MAX_LAYERS)
         return fail(MARF_ERR_UNSUPPORTED, "net_create: n_layers=%d (supported 2..%d)", n_layers, MARF_MAX_LAYERS);
-    if (dtype != MARF_FP32 && dtype != MARF_BF16) return fail(MARF_ERR_INVALID, "net_create: dtype %d", dtype);
+    if (dtype != MARF_FP32 && dtype != MARF_BF16 && dtype != MARF_BF16X3)
+        return fail(MARF_ERR_INVALID, "net_create: dtype %d", dtype);
     if (L < 0 || L > 32) return fail(MARF_ERR_UNSUPPORTED, "net_create: L=%d (supported 0..32)", L);
     int D = L > 0 ? 2 + 4 * L : 2;
     if (dims[0] != D) return fail(MARF_ERR_INVALID, "net_create: dims[0]=%d but 2+4L=%d", dims[0], D);
@@ -202,7 +261,8 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
     n->L = L;
     n->D = D;
     n->dtype = dtype;
-    n->elem = dtype == MARF_BF16 ? 2 : 4;
+    n->kdt = dtype == MARF_FP32 ? 0 : 1;
+    n->elem = n->kdt == 1 ? 2 : 4;
     for (int i = 0; i <= n_layers; ++i) {
         if (dims[i] <= 0) {
             delete n;
@@ -219,15 +279,15 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
         hmax = std::max(hmax, n->Mp[l]);
     }
     n->Mp[n_layers - 1] = 16;
-    n->Mt[n_layers - 1] = dtype == MARF_BF16 ? 16 : 4;
+    n->Mt[n_layers - 1] = n->kdt == 1 ? 16 : 4;
     n->Kmax = 0;
     for (int l = 0; l < n_layers; ++l) n->Kmax = std::max(n->Kmax, n->Kp[l]);
     if (hmax > 512 || n->Kmax > 512) {
         delete n;
         return fail(MARF_ERR_UNSUPPORTED, "net_create: hidden width %d > 512", hmax);
     }
-    n->TP = (dtype == MARF_BF16 && n->Kmax <= 256) ? 128 : 64;
-    n->lda = dtype == MARF_BF16 ? n->Kmax + 8 : n->Kmax + 1;
+    n->TP = (n->kdt == 1 && n->Kmax <= 256) ? 128 : 64;
+    n->lda = n->kdt == 1 ? n->Kmax + 8 : n->Kmax + 1;
     size_t act = (size_t)n->TP * n->lda * n->elem;
     size_t df = (size_t)n->TP * (n->Kp[0] + 1) * 4;
     n->lds_fwd = act;
@@ -253,6 +313,13 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
     }
     n->param_count = off;
     n->packed_bytes = boff;
+    plan_step2_net(n);
+    if (n->s2.variant >= 0) n->packed_bytes = n->s2.end_off;
+    if (dtype == MARF_BF16X3 && n->s2.variant < 0) {
+        delete n;
+        return fail(MARF_ERR_UNSUPPORTED,
+                    "net_create: split-bf16 needs <= 5 layers, hidden widths <= 256 and L <= 32");
+    }
     *out = n;
     return MARF_OK;
 }
@@ -282,7 +349,34 @@ int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, vo
         mx = std::max(mx, (long long)p.Mp * p.Kp + (long long)p.Kp * p.Mt + p.Mp);
     }
     MarfProfScope ps("pack_weights", (hipStream_t)stream);
-    HIPCHK(marf_launch_pack(net->dtype, d_params, (char*)d_packed, a, mx, (hipStream_t)stream), "net_pack");
+    HIPCHK(marf_launch_pack(net->kdt, d_params, (char*)d_packed, a, mx, (hipStream_t)stream), "net_pack");
+    if (net->s2.variant >= 0) {
+        const Step2NetPlan& q = net->s2;
+        Pack2Args b;
+        memset(&b, 0, sizeof(b));
+        b.nl = net->n_layers;
+        b.L = net->L;
+        b.nk0 = q.nk0;
+        b.nta = q.nta;
+        b.NKH = q.HM / 16;
+        b.split = q.variant == 1;
+        b.slot_bytes = q.slot;
+        b.n_stages = q.n_stages;
+        for (int l = 0; l <= net->n_layers; ++l) b.dims[l] = net->dims[l];
+        for (int l = 0; l < net->n_layers; ++l) {
+            b.nrt[l] = q.nrt[l];
+            b.nrtb[l] = q.nrtb[l];
+            b.w_off[l] = net->w_off[l];
+            b.b_off[l] = net->b_off[l];
+            b.boff[l] = q.boff[l];
+            b.Mp[l] = net->Mp[l];
+        }
+        b.nbias = q.nbias;
+        char* pk = (char*)d_packed;
+        HIPCHK(marf_launch_pack2(d_params, pk + q.prog_off, (float*)(pk + q.bias_off), (int*)(pk + q.kmap_off), b,
+                                 (hipStream_t)stream),
+               "net_pack step2");
+    }
     return MARF_OK;
 }
 
@@ -401,7 +495,7 @@ int marf_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* 
     int n_tiles = (int)(a.S / net->TP);
     {
         MarfProfScope ps("mlp_fwd", (hipStream_t)stream);
-        HIPCHK(marf_launch_mlp_fwd(a, net->dtype, net->TP, net->lds_fwd, n_tiles, (hipStream_t)stream), "forward");
+        HIPCHK(marf_launch_mlp_fwd(a, net->kdt, net->TP, net->lds_fwd, n_tiles, (hipStream_t)stream), "forward");
     }
     return MARF_OK;
 }
@@ -445,7 +539,7 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
     }
     {
         MarfProfScope ps("mlp_bwd_dgrad", s);
-        HIPCHK(marf_launch_mlp_bwd(a, net->dtype, net->TP, net->lds_bwd, n_tiles, s), "backward dgrad");
+        HIPCHK(marf_launch_mlp_bwd(a, net->kdt, net->TP, net->lds_bwd, n_tiles, s), "backward dgrad");
     }
 
     if (d_dparams) {
@@ -455,7 +549,7 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
         for (int l = 0; l < nl - 1; ++l) {
             {
                 MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
-                HIPCHK(marf_launch_wgrad(net->dtype, ws + wp.dz[l + 1], net->Kp[l + 1], sv + sp.feat[l], net->Kp[l],
+                HIPCHK(marf_launch_wgrad(net->kdt, ws + wp.dz[l + 1], net->Kp[l + 1], sv + sp.feat[l], net->Kp[l],
                                          a.S, net->Mp[l], net->Kp[l], wp.chunk, wp.n_chunks, part, bpart, s),
                        "backward wgrad");
             }
@@ -469,7 +563,7 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
         const int l = nl - 1;
         {
             MarfProfScope ps("wgrad_last", s);
-            HIPCHK(marf_launch_wgrad_last(net->dtype, a.glast, sv + sp.feat[l], a.S, net->Kp[l], net->Kp[l],
+            HIPCHK(marf_launch_wgrad_last(net->kdt, a.glast, sv + sp.feat[l], a.S, net->Kp[l], net->Kp[l],
                                           wp.chunk_last, wp.n_chunks_last, part, bpart, s),
                    "backward wgrad last");
         }
@@ -535,9 +629,216 @@ static void plan_step(const marf_net* n, long long S, StepPlan& p) {
     p.total = off;
 }
 
+// ---- the pixel-per-wave fused step (marf_step2.hip)
+
+struct Step2BufPlan {
+    size_t feat[MARF_MAX_LAYERS], dz[MARF_MAX_LAYERS];
+    size_t dH, loss, blast, wlast, dummy, c2f, kmap, part, bpart, total;
+    int grid, n_tiles;
+    long long S;
+};
+
+static int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        cus[dev] = c;
+    }
+    return cus[dev];
+}
+
+static bool use_step2(const marf_net* n) {
+    if (n->s2.variant < 0) return false;
+    if (n->s2.variant != 1 && !step2_env_enabled()) return false;
+    return true;
+}
+
+static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p) {
+    const Step2NetPlan& q = n->s2;
+    const int nl = n->n_layers;
+    p.S = (long long)g.B * g.Np_pad;
+    p.n_tiles = (int)(p.S / (32 * q.NW));
+    int cap = device_cus();
+    if (const char* e = getenv("MARF_STEP2_GRID")) cap = std::max(1, atoi(e));  // diagnostic override
+    p.grid = std::max(1, std::min(p.n_tiles, cap));
+    size_t off = 0;
+    for (int l = 0; l < nl - 1; ++l) {
+        p.feat[l] = off;
+        off += rup(p.S * (l == 0 ? q.ldf0 : n->Kp[l]) * 2, 256);
+    }
+    p.dz[0] = 0;
+    for (int l = 1; l < nl; ++l) {
+        p.dz[l] = off;
+        off += rup(p.S * n->Kp[l] * 2, 256);
+    }
+    p.dH = off;
+    off += rup(p.S / 32 * 9 * 4, 256);
+    p.loss = off;
+    off += rup((long long)p.grid * 2 * 8, 256);
+    p.blast = off;
+    off += rup((long long)p.grid * 3 * 4, 256);
+    p.wlast = off;
+    off += rup((long long)p.grid * 3 * q.Kl * 4, 256);
+    p.dummy = off;
+    off += rup((long long)p.grid * q.NW * 4 * 64 * 2 * 4, 256);
+    p.c2f = off;
+    off += 256;
+    p.kmap = off;  // the layer-0 column map, copied from the packed buffer by the forward
+    off += rup((long long)n->D * 4, 256);
+    // split-K partials of the hidden / layer-0 weight gradients (as plan_step)
+    long long chunk = rup((p.S + 255) / 256, 64);
+    if (chunk < 64) chunk = 64;
+    const long long n_chunks = (p.S + chunk - 1) / chunk;
+    long long mxo = 0, mxm = 0;
+    for (int l = 0; l < nl - 1; ++l) {
+        mxo = std::max(mxo, (long long)n->Mp[l] * (l == 0 ? q.ldf0 : n->Kp[l]));
+        mxm = std::max(mxm, (long long)n->Mp[l]);
+    }
+    p.part = off;
+    off += rup(std::max(n_chunks * mxo, 256LL * (3 * q.Kl + 3)) * 4, 256);
+    p.bpart = off;
+    off += rup(n_chunks * mxm * 4, 256);
+    p.total = off;
+}
+
+static int step2_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
+                         const float* d_gt, const float* d_mask, const float* d_denom_override, float* d_rgb,
+                         float* d_loss_out, void* d_saved, hipStream_t s) {
+    const Step2NetPlan& q = net->s2;
+    Step2Args a;
+    memset(&a, 0, sizeof(a));
+    int rc = make_geo(geo, a.geo, 32 * q.NW);
+    if (rc) return rc;
+    Step2BufPlan p;
+    plan_step2_bufs(net, a.geo, p);
+    char* sv = (char*)d_saved;
+    const char* pk = (const char*)d_packed;
+    const int nl = net->n_layers;
+    a.nl = nl;
+    a.L = net->L;
+    a.nk0 = q.nk0;
+    a.nta = q.nta;
+    C2fDev cf = make_c2f(c2f);
+    a.c2f_on = cf.on;
+    a.prog = pk + q.prog_off;
+    a.n_stages = q.n_stages;
+    a.bias = (const float*)(pk + q.bias_off);
+    a.nbias = q.nbias;
+    a.gt = d_gt;
+    a.mask = d_mask;
+    a.rgb = d_rgb;
+    for (int l = 0; l < nl; ++l) {
+        S2Layer& y = a.layers[l];
+        y.nrt = q.nrt[l];
+        y.nrtb = q.nrtb[l];
+        y.boff = q.boff[l];
+        y.ldf = l == 0 ? q.ldf0 : net->Kp[l];
+        y.ldz = net->Kp[l];
+        y.feat = l < nl - 1 ? (u16*)(sv + p.feat[l]) : nullptr;
+        y.dz = l >= 1 ? (u16*)(sv + p.dz[l]) : nullptr;
+    }
+    a.dH_partial = (float*)(sv + p.dH);
+    a.loss_partial = (double*)(sv + p.loss);
+    a.blast_partial = (float*)(sv + p.blast);
+    a.wlast_partial = (float*)(sv + p.wlast);
+    a.Kl = q.Kl;
+    a.c2f_w = (const float*)(sv + p.c2f);
+    a.dummy = (float*)(sv + p.dummy);
+    a.n_tiles = p.n_tiles;
+    // LDS layout
+    const int TPX = 32 * q.NW;
+    int off = 3 * q.slot;
+    a.lds_pro = off;
+    off += 2 * (4 * TPX + 64) * 4;
+    a.lds_bias = off;
+    off += (int)rup(q.nbias * 4, 16);
+    a.lds_c2f = off;
+    off += 128;
+    a.lds_layers = off;
+    off += (int)sizeof(S2Layer) * MARF_MAX_LAYERS;
+    a.lds_wave = off;
+    a.lds_wave_bytes = (int)rup(2048 + q.MAXR * q.NMW * 256 + 12 * q.Kl, 16);
+    off += q.NW * a.lds_wave_bytes;
+    a.lds_total = off;
+    if (off > 160 * 1024) return fail(MARF_ERR_UNSUPPORTED, "step2: LDS plan %d B exceeds 160 KB", off);
+    if (net->L > 0) HIPCHK(marf_launch_c2f_weights(cf, net->L, (float*)(sv + p.c2f), s), "step_forward c2f");
+    HIPCHK(hipMemcpyAsync(sv + p.kmap, pk + q.kmap_off, (size_t)net->D * 4, hipMemcpyDeviceToDevice, s),
+           "step_forward kmap");
+    {
+        MarfProfScope ps("mlp_step", s);
+        HIPCHK(marf_launch_step2(a, q.variant, p.grid, s), "step_forward step2");
+    }
+    {
+        MarfProfScope ps("loss_final", s);
+        HIPCHK(marf_launch_loss_final(a.loss_partial, p.grid, d_loss_out, d_denom_override, s), "step_forward loss");
+    }
+    return MARF_OK;
+}
+
+static int step2_backward(const marf_net* net, const marf_geometry* geo, const void* d_saved,
+                          const float* d_h_params, int lie_batch, const float* d_gout, const float* d_loss_out,
+                          float* d_dparams, float* d_dh, hipStream_t s) {
+    const Step2NetPlan& q = net->s2;
+    GeoDev g;
+    int rc = make_geo(geo, g, 32 * q.NW);
+    if (rc) return rc;
+    Step2BufPlan p;
+    plan_step2_bufs(net, g, p);
+    const char* sv = (const char*)d_saved;
+    float* part = (float*)(sv + p.part);
+    float* bpart = (float*)(sv + p.bpart);
+    const float* denom = d_loss_out + 1;
+    const int nl = net->n_layers;
+    if (d_dparams) {
+        long long chunk = rup((p.S + 255) / 256, 64);
+        if (chunk < 64) chunk = 64;
+        const int n_chunks = (int)((p.S + chunk - 1) / chunk);
+        const int* kmap = (const int*)(sv + p.kmap);
+        for (int l = 0; l < nl - 1; ++l) {
+            const int K = l == 0 ? q.ldf0 : net->Kp[l];
+            {
+                MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
+                HIPCHK(marf_launch_wgrad(1, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K,
+                                         (int)chunk, n_chunks, part, bpart, s),
+                       "step_backward wgrad");
+            }
+            {
+                MarfProfScope ps("wgrad_reduce", s);
+                HIPCHK(marf_launch_wgrad_reduce(part, bpart, n_chunks, net->Mp[l], K, net->dims[l + 1], net->dims[l],
+                                                d_dparams + net->w_off[l], d_dparams + net->b_off[l], s, d_gout, denom,
+                                                nullptr, l == 0 ? kmap : nullptr),
+                       "step_backward wgrad reduce");
+            }
+        }
+        const int l = nl - 1;
+        MarfProfScope ps("wgrad_last_reduce", s);
+        HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.wlast), (const float*)(sv + p.blast), p.grid, 3, q.Kl, 3,
+                                        net->dims[l], d_dparams + net->w_off[l], d_dparams + net->b_off[l], s, d_gout,
+                                        denom, part),
+               "step_backward last reduce");
+    }
+    if (d_dh) {
+        MarfProfScope ps("warp_bwd", s);
+        HIPCHK(marf_launch_reduce_dH((const float*)(sv + p.dH), g.Np_pad / 32, g.B, d_h_params, nullptr, d_dh,
+                                     lie_batch > 0 ? lie_batch : g.B, s, d_gout, denom),
+               "step_backward warp");
+    }
+    return MARF_OK;
+}
+
 size_t marf_step_saved_bytes(const marf_net* net, const marf_geometry* geo) {
     GeoDev g;
-    if (!net || !geo || geo->mode == MARF_GEO_COORDS || make_geo(geo, g, MARF_TILE_PAD) != MARF_OK) return 0;
+    if (!net || !geo || geo->mode == MARF_GEO_COORDS) return 0;
+    if (use_step2(net)) {
+        if (make_geo(geo, g, 32 * net->s2.NW) != MARF_OK) return 0;
+        Step2BufPlan p2;
+        plan_step2_bufs(net, g, p2);
+        return p2.total;
+    }
+    if (make_geo(geo, g, MARF_TILE_PAD) != MARF_OK) return 0;
     StepPlan p;
     plan_step(net, (long long)g.B * g.Np_pad, p);
     return p.total;
@@ -549,6 +850,8 @@ int marf_step_forward(const marf_net* net, const marf_geometry* geo, const marf_
     if (!net || !d_packed || !d_gt || !d_loss_out || !d_saved) return fail(MARF_ERR_INVALID, "step_forward: NULL argument");
     if (!geo || geo->mode == MARF_GEO_COORDS) return fail(MARF_ERR_INVALID, "step_forward: needs a pixel-grid geometry");
     hipStream_t s = (hipStream_t)stream;
+    if (use_step2(net))
+        return step2_forward(net, geo, c2f, d_packed, d_gt, d_mask, d_denom_override, d_rgb, d_loss_out, d_saved, s);
     StepArgs a;
     memset(&a, 0, sizeof(a));
     int rc = make_geo(geo, a.geo, MARF_TILE_PAD);
@@ -578,7 +881,7 @@ int marf_step_forward(const marf_net* net, const marf_geometry* geo, const marf_
     if (net->L > 0) HIPCHK(marf_launch_c2f_weights(a.c2f, net->L, (float*)(sv + p.c2f), s), "step_forward c2f");
     {
         MarfProfScope ps("mlp_step", s);
-        HIPCHK(marf_launch_mlp_step(a, net->dtype, net->TP, net->lds_step, p.n_tiles, s), "step_forward");
+        HIPCHK(marf_launch_mlp_step(a, net->kdt, net->TP, net->lds_step, p.n_tiles, s), "step_forward");
     }
     {
         MarfProfScope ps("loss_final", s);
@@ -594,6 +897,7 @@ int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void
     if (!geo || geo->mode == MARF_GEO_COORDS) return fail(MARF_ERR_INVALID, "step_backward: needs a pixel-grid geometry");
     if (d_dh && !d_h_params) return fail(MARF_ERR_INVALID, "step_backward: d_dh requested without the warp parameters");
     hipStream_t s = (hipStream_t)stream;
+    if (use_step2(net)) return step2_backward(net, geo, d_saved, d_h_params, lie_batch, d_gout, d_loss_out, d_dparams, d_dh, s);
     GeoDev g;
     int rc = make_geo(geo, g, MARF_TILE_PAD);
     if (rc) return rc;
@@ -609,7 +913,7 @@ int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void
         for (int l = 0; l < nl - 1; ++l) {
             {
                 MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
-                HIPCHK(marf_launch_wgrad(net->dtype, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], net->Kp[l], S,
+                HIPCHK(marf_launch_wgrad(net->kdt, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], net->Kp[l], S,
                                          net->Mp[l], net->Kp[l], p.chunk, p.n_chunks, part, bpart, s),
                        "step_backward wgrad");
             }

@@ -70,6 +70,51 @@ struct PackArgs {
     PackLayer ly[MARF_MAX_LAYERS];
 };
 
+// Per-layer constants, copied into LDS at kernel start (kept out of the SGPR file).
+struct S2Layer {
+    int nrt;     // row tiles of the forward output (Mp / 32; last layer: 1)
+    int nrtb;    // row tiles of the dgrad output (Kp / 32; layer 0: the adjoint tiles)
+    int boff;    // offset of the padded bias in the bias table
+    int ldf;     // row stride of feat_l (elements)
+    int ldz;     // row stride of dz_l
+    int pad;
+    u16* feat;   // feat_l [S][ldf] bf16 (l = 0 .. nl-2)
+    u16* dz;     // dz_l [S][ldz] bf16 (l = 1 .. nl-1)
+};
+
+struct Step2Args {
+    GeoDev geo;                      // Np_pad is a multiple of 32 * NW
+    int nl, L, nk0, nta, c2f_on;
+    const char* prog;                // weight stage program: n_stages slots of SLOT bytes
+    int n_stages;
+    const float* bias;               // padded biases
+    int nbias;                       // floats in the bias table
+    const float* gt;                 // [B][3][Np]
+    const float* mask;               // [B][1][Np] or null
+    float* rgb;                      // [B][Np][3] or null
+    S2Layer layers[MARF_MAX_LAYERS]; // per-layer table (copied into LDS at kernel start)
+    float* dH_partial;               // [S / 32][9]
+    double* loss_partial;            // [grid][2]
+    float* blast_partial;            // [grid][3]
+    float* wlast_partial;            // [grid][3][Kl]
+    int Kl;                          // padded input width of the last layer
+    const float* c2f_w;              // [L] band weights of this step
+    float* dummy;                    // [grid][NW][ST][64][2] store sink
+    int n_tiles;                     // block tiles of 32 * NW pixel slots
+    // LDS layout (byte offsets; computed on the host)
+    int lds_pro, lds_bias, lds_c2f, lds_layers, lds_wave, lds_wave_bytes, lds_total;
+};
+
+struct Pack2Args {
+    int nl, L, nk0, nta, NKH, split, slot_bytes, n_stages;
+    int dims[MARF_MAX_LAYERS + 1];   // true widths
+    int nrt[MARF_MAX_LAYERS], nrtb[MARF_MAX_LAYERS];
+    long long w_off[MARF_MAX_LAYERS], b_off[MARF_MAX_LAYERS];  // flat parameter offsets
+    int boff[MARF_MAX_LAYERS];       // padded bias table offsets
+    int Mp[MARF_MAX_LAYERS];
+    int nbias;
+};
+
 // Raise a kernel's dynamic-LDS limit to at least `lds` bytes before a launch.  The limit set so
 // far is tracked per (device, kernel) under a mutex, so a later launch of the same instantiation
 // with a larger tile (a wider net) raises it again, and concurrent host threads do not race.
@@ -90,10 +135,14 @@ hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* fea
                                   int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s);
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
                                     int Ko, float* dW, float* db, hipStream_t s, const float* gscale = nullptr,
-                                    const float* denom = nullptr, float* scratch = nullptr);
+                                    const float* denom = nullptr, float* scratch = nullptr,
+                                    const int* kmap = nullptr);
 hipError_t marf_launch_mlp_step(const marf::StepArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
 hipError_t marf_launch_c2f_weights(const marf::C2fDev& c, int L, float* out, hipStream_t s);
 hipError_t marf_launch_loss_final(const double* part, int n, float* out, const float* denom_override, hipStream_t s);
+hipError_t marf_launch_step2(const marf::Step2Args& a, int variant, int grid, hipStream_t s);
+hipError_t marf_launch_pack2(const float* params, void* prog, float* bias_out, int* kmap, const marf::Pack2Args& a,
+                             hipStream_t s);
 hipError_t marf_launch_edge_map(const float* in, double* out, int n_img, int H, int W, hipStream_t s);
 hipError_t marf_launch_erode_rect(const float* in, float* out, int n_img, int H, int W, int kh, int kw, hipStream_t s);
 hipError_t marf_launch_mse(const float* pred, const float* gt, const float* mask, int B, int Np, double* part,

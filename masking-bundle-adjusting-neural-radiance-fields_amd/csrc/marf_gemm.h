@@ -33,7 +33,11 @@ MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int col
     } else {
         for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
             int r = e / cols, c = e - r * cols;
+#if defined(MARF_DIAG_SAVE_BF16)
+            dst[(size_t)r * ldd + c] = diag_round_bf16(act[(size_t)r * lda + c]);
+#else
             dst[(size_t)r * ldd + c] = act[(size_t)r * lda + c];
+#endif
         }
     }
 }

@@ -163,7 +163,11 @@ __global__ void k_pack(const float* __restrict__ params, char* __restrict__ pack
         } else if (e < nf + nt) {
             int kr, m;  // row of W^T = input feature, column = output feature
             frag_coord<P>(e - nf, nkt, false, kr, m);
-            wt[e - nf] = P::cvt(m < L.M && kr < L.K ? W[(size_t)m * L.K + kr] : 0.f);
+            float wtv = m < L.M && kr < L.K ? W[(size_t)m * L.K + kr] : 0.f;
+#if defined(MARF_DIAG_WT_BF16)
+            wtv = diag_round_bf16(wtv);
+#endif
+            wt[e - nf] = P::cvt(wtv);
         } else {
             int m = (int)(e - nf - nt);
             bias[m] = m < L.M ? bsrc[m] : 0.f;

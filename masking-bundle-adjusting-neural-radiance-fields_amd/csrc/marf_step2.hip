@@ -1,0 +1,851 @@
+// marf_step2.hip -- the fused training step in the pixel-per-wave form (gfx950).
+//
+// Same contract as k_mlp_step (marf_step.hip): per pixel grid -> sl(3) warp -> posenc + c2f ->
+// MLP forward -> sigmoid -> masked-MSE partial -> d rgb -> dgrad chain -> posenc / warp adjoint,
+// writing the layer inputs feat_l and the pre-activation gradients dz_l that the weight-gradient
+// kernels (marf_wgrad.hip) consume (model/planar.py:329-391, warp.py:33-81).  The mapping onto the
+// CU is different:
+//
+//   * one wave owns 32 pixels and computes EVERY feature of them; a 32x32 accumulator tile of
+//     layer l (rows = features, column = the lane's pixel) is, after ReLU and bf16 packing, the B
+//     operand of layer l+1 as it stands (CDNA "accumulator as the next MFMA's operand": registers
+//     8s..8s+7 form k-step s, with the k order permuted inside the step).  Activations never touch
+//     LDS; the weights are packed in the matching k order.
+//   * the weights (MFMA A operand) stream through a 3-slot LDS ring shared by all waves of the
+//     block: one slot = one 32-row tile of one layer's matrix, filled by global_load_lds_dwordx4
+//     (issued by every wave, 1 KB per instruction) two stages ahead of its use.  The block is
+//     persistent (one per CU) and the per-tile stage sequence repeats, so the stream never stops
+//     between pixel tiles.
+//   * ReLU masks stay in registers from the forward to the backward (no mask records in HBM).
+//   * split-bf16 mode (MARF_BF16X3): weights and forward activations are carried as bf16 hi + lo
+//     pairs, the forward is hi*hi + hi*lo + lo*hi (fp32 accumulation, ~16 significant bits) and
+//     the dgrad is W_hi^T dz + W_lo^T dz; dz and the saved tensors stay bf16.  This is the precision
+//     recipe that keeps the seed-3 planar run in the reference's basin.
+//
+// Memory ordering: all global traffic inside the tile loop is inline asm (LDS-DMA, stores) so the
+// compiler inserts no vmcnt waits of its own; every stage issues exactly ST store instructions
+// (padding with stores to a per-wave scratch line), so the wait for a ring slot is one constant
+// vmcnt (D * ST + (D - 1) * PER_DMA younger operations).
+#include <type_traits>
+
+#include "marf_args.h"
+
+namespace marf {
+
+// ------------------------------------------------------------------ inline-asm memory ops
+
+// LDS-DMA, 16 B per lane (1 KB per wave instruction), lds = wave-uniform LDS byte address
+MARF_DEV void s2_glds16(const void* src, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
+}
+// LDS-DMA, 4 B per lane (256 B per wave instruction)
+MARF_DEV void s2_glds4(const void* src, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
+}
+// Stores outside the compiler's bookkeeping: the s_nop covers the store-data hazard (the data
+// registers may be rewritten right after), which hipcc pads only for its own stores.
+typedef uint32_t s2_u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t s2_u32x4 __attribute__((ext_vector_type(4)));
+MARF_DEV void s2_st8(void* dst, uint32_t a, uint32_t b) {
+    const s2_u32x2 v = {a, b};
+    asm volatile("global_store_dwordx2 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
+}
+MARF_DEV void s2_st16(void* dst, uint4 u) {
+    const s2_u32x4 v = {u.x, u.y, u.z, u.w};
+    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
+}
+MARF_DEV void s2_st12(void* dst, float a, float b, float c) {
+    typedef float f32x3 __attribute__((ext_vector_type(3)));
+    f32x3 v = {a, b, c};
+    asm volatile("global_store_dwordx3 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
+}
+MARF_DEV void s2_st4(void* dst, float a) {
+    asm volatile("global_store_dword %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(a) : "memory");
+}
+template <int N>
+MARF_DEV void s2_wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+MARF_DEV i16x4 s2_tr16(const u16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
+}
+
+// two floats -> packed bf16 pair (v_cvt_pk_bf16_f32, RNE)
+MARF_DEV uint32_t s2_pk(float a, float b) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){a, b}), bf16x2));
+}
+MARF_DEV float s2_lo16(uint32_t w) { return __uint_as_float(w << 16); }
+MARF_DEV float s2_hi16(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+union S2Frag {
+    bf16x8 f;
+    uint4 u;
+};
+
+// 8 floats -> bf16 hi fragment (+ lo remainder fragment)
+template <bool LO>
+MARF_DEV void s2_split8(const float* x, S2Frag& hi, S2Frag& lo) {
+    hi.u = make_uint4(s2_pk(x[0], x[1]), s2_pk(x[2], x[3]), s2_pk(x[4], x[5]), s2_pk(x[6], x[7]));
+    if constexpr (LO) {
+        const uint32_t w[4] = {hi.u.x, hi.u.y, hi.u.z, hi.u.w};
+        float r[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            r[2 * q] = x[2 * q] - s2_lo16(w[q]);
+            r[2 * q + 1] = x[2 * q + 1] - s2_hi16(w[q]);
+        }
+        lo.u = make_uint4(s2_pk(r[0], r[1]), s2_pk(r[2], r[3]), s2_pk(r[4], r[5]), s2_pk(r[6], r[7]));
+    }
+}
+
+// ------------------------------------------------------------------ the kernel
+
+template <int HM, bool SPLIT, int NW, int MAXR>
+struct S2Cfg {
+    static constexpr int NKH = HM / 16;                    // k-steps of a hidden-width operand
+    static constexpr int NRT = HM / 32;                    // row tiles of a hidden-width output
+    static constexpr int SLOT = NKH * 1024 * (SPLIT ? 2 : 1);
+    static constexpr int LO = NKH * 1024;                  // byte offset of the lo fragments in a slot
+    static constexpr int PER_DMA = SLOT / (NW * 1024);     // DMA instructions per wave per stage
+    static constexpr int NSLOT = 3, D = 2;
+    static constexpr int ST = 4;                           // store instructions per wave per stage
+    static constexpr int NK0 = 9;                          // max layer-0 k-steps (L <= 32)
+    static constexpr int NTA = 5;                          // max adjoint row tiles (L <= 39)
+    static constexpr int TPX = 32 * NW;                    // pixel slots per block tile
+    static constexpr int NMW = NRT / 2;                    // mask words per ReLU layer
+    static_assert(PER_DMA * NW * 1024 == SLOT, "slot size");
+};
+
+template <int HM, bool SPLIT, int NW, int MAXR>
+__global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
+    typedef S2Cfg<HM, SPLIT, NW, MAXR> C;
+    constexpr int NKH = C::NKH, NRT = C::NRT, ST = C::ST;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5, pxl = lane & 31;
+    const int nl = a.nl, L = a.L;
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    float* bias_l = reinterpret_cast<float*>(smem + a.lds_bias);
+    float* c2f_l = reinterpret_cast<float*>(smem + a.lds_c2f);
+    S2Layer* lyr = reinterpret_cast<S2Layer*>(smem + a.lds_layers);
+    auto ly_int = [&](int l, int field) -> int {
+        return __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(lyr + l)[field]);
+    };
+    auto ly_ptr = [&](int l, int which) -> u16* {  // which 0: feat, 1: dz
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(lyr + l) + 6 + 2 * which;
+        const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane(q[0]);
+        const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane(q[1]);
+        return reinterpret_cast<u16*>(lo | (hi << 32));
+    };
+    char* wpriv = smem + a.lds_wave + wave * a.lds_wave_bytes;
+    u16* trs = reinterpret_cast<u16*>(wpriv);                 // 1 KB transpose scratch
+    u16* gts = reinterpret_cast<u16*>(wpriv + 1024);          // 1 KB g^T image [16][32]
+    uint32_t* mkl = reinterpret_cast<uint32_t*>(wpriv + 2048);  // ReLU mask words [MAXR][NMW][64]
+    float* wla = reinterpret_cast<float*>(wpriv + 2048 + MAXR * C::NMW * 256);  // [3][Kl] dW_last
+    float* dmy = a.dummy + (((size_t)blockIdx.x * NW + wave) * ST * 64 + lane) * 2;
+
+    // ---- constants into LDS (plain loads: the compiler's waits are harmless before the ring)
+    for (int e = threadIdx.x; e < a.nbias; e += NW * 64) bias_l[e] = a.bias[e];
+    if ((int)threadIdx.x < 32) c2f_l[threadIdx.x] = (int)threadIdx.x < L ? a.c2f_w[threadIdx.x] : 0.f;
+    for (int e = threadIdx.x; e < nl * (int)(sizeof(S2Layer) / 4); e += NW * 64)
+        reinterpret_cast<uint32_t*>(lyr)[e] = reinterpret_cast<const uint32_t*>(a.layers)[e];
+    for (int e = lane; e < 512; e += 64) reinterpret_cast<uint32_t*>(gts)[e] = 0u;
+    for (int e = lane; e < 3 * a.Kl; e += 64) wla[e] = 0.f;
+
+    const int tpp = a.geo.Np_pad / C::TPX;   // block tiles per patch
+    const int Np = a.geo.Np;
+    int my_tiles = 0;
+    if ((int)blockIdx.x < a.n_tiles) my_tiles = (a.n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
+    const int total = my_tiles * a.n_stages;
+
+    // ---- per-tile input DMA: target r, g, b, mask (TPX floats each) and H (9 floats) of a tile
+    auto pro_buf = [&](int pb) -> float* { return reinterpret_cast<float*>(smem + a.lds_pro + pb * (4 * C::TPX + 64) * 4); };
+    auto issue_pro = [&](int tile, int pb) {
+        const int b = tile / tpp, q0 = (tile - b * tpp) * C::TPX;
+        const unsigned base = lds0 + a.lds_pro + pb * (4 * C::TPX + 64) * 4;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int f = ((wave * 2 + i) * 64) + lane;   // float index in [0, 4 TPX)
+            const int ch = f / C::TPX, q = f - ch * C::TPX;
+            const int p = min(q0 + q, Np - 1);
+            const float* src = ch < 3 ? a.gt + ((size_t)b * 3 + ch) * Np + p
+                                      : (a.mask ? a.mask + (size_t)b * Np + p : a.gt + (size_t)b * 3 * Np + p);
+            s2_glds4(src, __builtin_amdgcn_readfirstlane(base + (wave * 2 + i) * 256));
+        }
+        s2_glds4(a.geo.Hm + 9 * (size_t)b + (lane < 9 ? lane : 0), __builtin_amdgcn_readfirstlane(base + 4 * C::TPX * 4));
+    };
+
+    // ---- the weight ring
+    int c_stage = 0;         // global stage counter of this block
+    int dma_stage = 0;       // next stage whose DMA is to be issued
+    int dma_prog = 0;        // its index in the program
+    auto issue_stage = [&]() {
+        const unsigned dst = lds0 + (dma_stage % C::NSLOT) * C::SLOT;
+        const char* src = a.prog + (size_t)dma_prog * C::SLOT;
+#pragma unroll
+        for (int i = 0; i < C::PER_DMA; ++i) {
+            const int piece = wave * C::PER_DMA + i;
+            s2_glds16(src + piece * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(dst + piece * 1024));
+        }
+        ++dma_stage;
+        if (++dma_prog == a.n_stages) dma_prog = 0;
+    };
+    // wait for stage c_stage, publish it to every wave, refill the slot freed by stage c_stage - 1
+    auto stage_begin = [&]() -> const char* {
+        if (c_stage + 1 < total) s2_wait_vm<C::D * ST + C::PER_DMA>();
+        else s2_wait_vm<C::D * ST>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (dma_stage < total) issue_stage();
+        const char* slot = smem + (c_stage % C::NSLOT) * C::SLOT;
+        ++c_stage;
+        return slot;
+    };
+
+    if (my_tiles > 0) {
+        issue_pro((int)blockIdx.x, 0);
+        if (dma_stage < total) issue_stage();
+        if (dma_stage < total) issue_stage();
+    }
+    s2_wait_vm<0>();
+    __syncthreads();
+
+    // running per-lane sums over this block's tiles (fixed order -> deterministic)
+    double lsq = 0.0, lms = 0.0;
+    float bl0 = 0.f, bl1 = 0.f, bl2 = 0.f;
+
+    // ReLU mask words in wave-private LDS: word (layer, rt >> 1) of a lane, bit
+    // (16 (1 - (rt & 1)) + 15 - r) = accumulator register r (the pair of row tiles is assembled in
+    // a register, so each word is written once)
+    uint32_t mpend = 0u;
+
+    S2Frag Bh[NKH], Bl[NKH], Oh[NKH], Ol[NKH];
+
+    auto dummies = [&](auto n_tag) {
+        constexpr int N = decltype(n_tag)::value;
+#pragma unroll
+        for (int i = 0; i < N; ++i) s2_st8(dmy + i * 128, 0u, 0u);
+    };
+    typedef std::integral_constant<int, ST> STt;
+    typedef std::integral_constant<int, ST - 1> ST1t;
+    // (the stores of a row tile into a natural-order [S][ld] bf16 tensor: k-step ks of the lane's
+    //  pixel holds columns 16 ks + 4 h + 0..3 (elements 0-3) and 16 ks + 8 + 4 h + 0..3 (4-7))
+    auto store_rt = [&](u16* base, int ld, long long slot, int rt, const S2Frag& f0, const S2Frag& f1) {
+        u16* row = base + slot * ld;
+        s2_st8(row + 32 * rt + 4 * h, f0.u.x, f0.u.y);
+        s2_st8(row + 32 * rt + 8 + 4 * h, f0.u.z, f0.u.w);
+        s2_st8(row + 32 * rt + 16 + 4 * h, f1.u.x, f1.u.y);
+        s2_st8(row + 32 * rt + 24 + 4 * h, f1.u.z, f1.u.w);
+    };
+
+    // one 32-row output tile: acc (+)= A[ks] . B[ks] over NK k-steps from the slot
+    //   MODE 0: plain; 1: split forward (hi.hi + hi.lo + lo.hi); 2: split dgrad (hi.B + lo.B)
+    auto gemm = [&](f32x16& acc, const char* slot, const S2Frag* Bhi, const S2Frag* Blo, int nk, auto mode_tag,
+                    auto nk_tag) {
+        constexpr int MODE = decltype(mode_tag)::value;
+        constexpr int NK = decltype(nk_tag)::value;
+        const bf16x8* ah = reinterpret_cast<const bf16x8*>(slot + lane * 16);
+        const bf16x8* al = reinterpret_cast<const bf16x8*>(slot + C::LO + lane * 16);
+        // 4-deep register ring of A fragments; sched_barrier pins the issue order (left alone the
+        // scheduler sinks each LDS read to right before its MFMA and exposes its latency)
+        constexpr int P = NK < 4 ? NK : 4;
+        bf16x8 A0[4], A1[4];
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            A0[u] = ah[u * 64];
+            if constexpr (MODE != 0) A1[u] = al[u * 64];
+        }
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks) {
+            const bool live = NK != C::NK0 || ks < nk;
+            const int u = ks & 3;
+            __builtin_amdgcn_sched_barrier(0);
+            if (live) {
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0[u], Bhi[ks].f, acc, 0, 0, 0);
+                if constexpr (MODE == 1) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0[u], Blo[ks].f, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[u], Bhi[ks].f, acc, 0, 0, 0);
+                } else if constexpr (MODE == 2) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[u], Bhi[ks].f, acc, 0, 0, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks + P < NK) {
+                A0[u] = ah[(ks + P) * 64];
+                if constexpr (MODE != 0) A1[u] = al[(ks + P) * 64];
+            }
+        }
+    };
+    typedef std::integral_constant<int, 0> M0t;
+    typedef std::integral_constant<int, SPLIT ? 1 : 0> MFt;
+    typedef std::integral_constant<int, SPLIT ? 2 : 0> MBt;
+    typedef std::integral_constant<int, NKH> NKHt;
+    typedef std::integral_constant<int, C::NK0> NK0t;
+    typedef std::integral_constant<int, 1> NK1t;
+
+    auto bias_init = [&](int boff, int rt) -> f32x16 {
+        f32x16 acc;
+        const float* bb = bias_l + boff + rt * 32 + 4 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 v = *reinterpret_cast<const float4*>(bb + 8 * q);
+            acc[4 * q] = v.x;
+            acc[4 * q + 1] = v.y;
+            acc[4 * q + 2] = v.z;
+            acc[4 * q + 3] = v.w;
+        }
+        return acc;
+    };
+    // forward epilogue: ReLU, mask bits, next-layer operand fragments (k-steps 2 rt, 2 rt + 1)
+    // row tiles past a narrower layer's width: zero operand fragments (the padded weights are zero,
+    // and 0 * stale bits could be NaN)
+    auto zero_out = [&](S2Frag& o0, S2Frag& o1, S2Frag& q0, S2Frag& q1) {
+        o0.u = o1.u = q0.u = q1.u = make_uint4(0, 0, 0, 0);
+    };
+    auto relu_out = [&](f32x16& acc, int l, int rt, S2Frag& o0, S2Frag& o1, S2Frag& q0, S2Frag& q1) {
+        uint32_t bits = 0;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float x;
+            asm volatile(
+                "v_cmp_lt_f32_e32 vcc, 0, %2\n\t"
+                "v_cndmask_b32_e32 %0, 0, %2, vcc\n\t"
+                "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+                : "=&v"(x), "+v"(bits)
+                : "v"(acc[r])
+                : "vcc");
+            v[r] = x;
+        }
+        if ((rt & 1) == 0) mpend = bits << 16;
+        else mkl[(l * C::NMW + (rt >> 1)) * 64 + lane] = mpend | bits;
+        s2_split8<SPLIT>(v, o0, q0);
+        s2_split8<SPLIT>(v + 8, o1, q1);
+    };
+    // dgrad epilogue: dz = acc * relu'(z) with the forward's mask word
+    auto mask_out = [&](f32x16& acc, int lmask, int rt, S2Frag& o0, S2Frag& o1) {
+        const uint32_t w = mkl[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = __builtin_amdgcn_sbfe((int)w, 16 * (1 - (rt & 1)) + 15 - r, 1);
+            v[r] = __int_as_float(__float_as_int(acc[r]) & m);
+        }
+        S2Frag dumm;
+        s2_split8<false>(v, o0, dumm);
+        s2_split8<false>(v + 8, o1, dumm);
+    };
+
+    const float pi_f = 3.14159265358979323846f;
+
+    for (int it = 0; it < my_tiles; ++it) {
+        const int tile = (int)blockIdx.x + it * (int)gridDim.x;
+        const int pb = it & 1;
+        const int b = tile / tpp;
+        const int p0 = (tile - b * tpp) * C::TPX + 32 * wave;
+        const long long slot0 = (long long)b * a.geo.Np_pad + p0;
+        const long long myslot = slot0 + pxl;
+        const int p = p0 + pxl;
+        const bool valid = p < Np;
+        const float* pro = pro_buf(pb);
+
+        // ---- prologue: pixel grid -> warp (warp.py:33-81) -> posenc + c2f features (model/planar.py:451-471)
+        float Hm[9];
+#pragma unroll
+        for (int e = 0; e < 9; ++e) Hm[e] = pro[4 * C::TPX + e];
+        float x, y, u, v, X[3];
+        {
+            const int r = p / a.geo.w, cc = p - r * a.geo.w;
+            x = grid_coord(a.geo.x0 + cc, a.geo.W, a.geo.norm_w);
+            y = grid_coord(a.geo.y0 + r, a.geo.H, a.geo.norm_h);
+            warp_point(Hm, x, y, u, v, X, a.geo.bmm_small);
+        }
+        const float cd = h ? v : u;
+        S2Frag F0h[C::NK0], F0l[C::NK0];
+        {
+            const int ng = a.nk0 - 1;  // band groups of 4
+#pragma unroll
+            for (int g = 0; g < C::NK0 - 1; ++g) {
+                if (g < ng) {
+                    float f[8];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int k = 4 * g + j;
+                        float s = 0.f, co = 0.f;
+                        if (k < L) {
+                            band_sincos<true>(cd, k, s, co);
+                            if (a.c2f_on) {
+                                const float w = c2f_l[k];
+                                s = s * w;
+                                co = co * w;
+                            }
+                        }
+                        f[j] = s;
+                        f[4 + j] = co;
+                    }
+                    s2_split8<SPLIT>(f, F0h[g], F0l[g]);
+                }
+            }
+            float f[8] = {cd, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            S2Frag rh, rl;
+            s2_split8<SPLIT>(f, rh, rl);
+#pragma unroll
+            for (int g = 0; g < C::NK0; ++g)
+                if (g == ng) {
+                    F0h[g] = rh;
+                    F0l[g] = rl;
+                }
+            // feat_0 (bf16 hi) for the layer-0 weight gradient: column 16 ks + 8 h + j
+            u16* row = ly_ptr(0, 0) + myslot * ly_int(0, 3);
+#pragma unroll
+            for (int g = 0; g < C::NK0; ++g)
+                if (g < a.nk0) s2_st16(row + 16 * g + 8 * h, F0h[g].u);
+            if (16 * a.nk0 < ly_int(0, 3)) s2_st16(row + 16 * a.nk0 + 8 * h, make_uint4(0, 0, 0, 0));
+        }
+
+        // ---- layer 0 forward
+        {
+            const int nrt = ly_int(0, 0);
+            const bool save = nl > 2;
+#pragma unroll
+            for (int rt = 0; rt < NRT; ++rt) {
+                if (rt < nrt) {
+                    const char* slot = stage_begin();
+                    // the next tile's target / mask / H into the other input buffer (the tile that
+                    // read it last finished before this stage's barrier)
+                    if (rt == 0 && it + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
+                    f32x16 acc = bias_init(ly_int(0, 2), rt);
+                    gemm(acc, slot, F0h, F0l, a.nk0, MFt(), NK0t());
+                    relu_out(acc, 0, rt, Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
+                    if (save) store_rt(ly_ptr(1, 0), ly_int(1, 3), myslot, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+                    else dummies(STt());
+                } else {
+                    zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NKH; ++k) {
+                Bh[k] = Oh[k];
+                if constexpr (SPLIT) Bl[k] = Ol[k];
+            }
+        }
+        // ---- hidden layers forward
+        for (int l = 1; l < nl - 1; ++l) {
+            const int nrt = ly_int(l, 0);
+            const bool save = l + 1 < nl - 1;
+#pragma unroll
+            for (int rt = 0; rt < NRT; ++rt) {
+                if (rt < nrt) {
+                    const char* slot = stage_begin();
+                    f32x16 acc = bias_init(ly_int(l, 2), rt);
+                    gemm(acc, slot, Bh, Bl, NKH, MFt(), NKHt());
+                    relu_out(acc, l, rt, Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
+                    if (save) store_rt(ly_ptr(l + 1, 0), ly_int(l + 1, 3), myslot, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+                    else dummies(STt());
+                } else {
+                    zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NKH; ++k) {
+                Bh[k] = Oh[k];
+                if constexpr (SPLIT) Bl[k] = Ol[k];
+            }
+        }
+
+        // ---- last layer: 3 outputs (rows 0..2 of one tile), sigmoid, masked MSE, d rgb
+        float g[3] = {0.f, 0.f, 0.f};
+        {
+            const char* slot = stage_begin();
+            f32x16 acc = bias_init(ly_int(nl - 1, 2), 0);
+            gemm(acc, slot, Bh, Bl, NKH, MFt(), NKHt());
+            float* o = (a.rgb && valid && h == 0) ? a.rgb + ((size_t)b * Np + p) * 3 : dmy;
+            float yv[3] = {0.f, 0.f, 0.f};
+            if (h == 0) {
+                const float m = valid ? (a.mask ? pro[3 * C::TPX + 32 * wave + pxl] : 1.0f) : 0.f;
+                double sq = 0.0;
+                float sqf = 0.f;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float z = acc[c];
+                    const float yy = 1.0f / (1.0f + expf(-z));
+                    yv[c] = yy;
+                    const float t = valid ? pro[c * C::TPX + 32 * wave + pxl] : 0.f;
+                    // model/planar.py:388-390 and its autograd: x = (p - g) m, d = 2 x m
+                    const float xx = (yy - t) * m;
+                    sqf += xx * xx;
+                    const float d = (2.0f * xx) * m;
+                    g[c] = (d * (1.0f - yy)) * yy;  // sigmoid backward
+                }
+                sq = (double)sqf;
+                lsq += sq;
+                lms += (double)m;
+                bl0 += g[0];
+                bl1 += g[1];
+                bl2 += g[2];
+            }
+            s2_st12(o, yv[0], yv[1], yv[2]);
+            dummies(ST1t());
+        }
+        // g operand of the last-layer dgrad: lane half 0, k = [g hi (3), 0, g lo (3), 0]
+        S2Frag Bg;
+        {
+            float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (h == 0) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    f[c] = g[c];                                        // bf16(g) below
+                    f[4 + c] = g[c] - s2_lo16(s2_pk(g[c], 0.f));         // g - bf16(g)
+                }
+            }
+            S2Frag dumm;
+            s2_split8<false>(f, Bg, dumm);
+        }
+        // ---- last-layer weight gradient of the wave's 32 pixels: dW[c][k] += sum_px g[c] feat[k]
+        //      16x16x32 MFMA: A = g^T (rows 0-2 hi, 4-6 lo; K = 32 pixels) from a wave-private
+        //      LDS image, B = feat^T per 16-feature k-step through a transposing LDS round trip
+        {
+            if (h == 0) {
+                const uint32_t w0 = Bg.u.x, w1 = Bg.u.y, w2 = Bg.u.z, w3 = Bg.u.w;
+                gts[0 * 32 + pxl] = (u16)(w0 & 0xffff);
+                gts[1 * 32 + pxl] = (u16)(w0 >> 16);
+                gts[2 * 32 + pxl] = (u16)(w1 & 0xffff);
+                gts[4 * 32 + pxl] = (u16)(w2 & 0xffff);
+                gts[5 * 32 + pxl] = (u16)(w2 >> 16);
+                gts[6 * 32 + pxl] = (u16)(w3 & 0xffff);
+            }
+            const bf16x8 ga = *reinterpret_cast<const bf16x8*>(gts + (lane & 15) * 32 + 8 * (lane >> 4));
+            const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+            const int nkl = a.Kl / 16;
+#pragma unroll
+            for (int ks = 0; ks < NKH; ++ks) {
+                if (ks < nkl) {
+                    *reinterpret_cast<uint4*>(trs + (pxl * 2 + h) * 8) = Bh[ks].u;
+                    const u16* b0 = trs + (8 * gq + q) * 16 + (pp & 1) * 8 + 4 * (pp >> 1);
+                    i16x4 vv[2] = {s2_tr16(b0), s2_tr16(b0 + 4 * 16)};
+                    const f32x4 r4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, *reinterpret_cast<bf16x8*>(vv), (f32x4){}, 0, 0, 0);
+                    float lo[3];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) lo[c] = __shfl_down(r4[c], 16, 64);
+                    if (lane < 16) {
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) wla[c * a.Kl + 16 * ks + lane] += r4[c] + lo[c];
+                    }
+                }
+            }
+        }
+
+        // ---- last-layer dgrad: dfeat_{n-1} = W_{n-1}^T g, mask -> dz_{n-1}
+        {
+            const int nrt = ly_int(nl - 1, 1);
+            S2Frag gB[1] = {Bg};
+#pragma unroll
+            for (int rt = 0; rt < NRT; ++rt) {
+                if (rt < nrt) {
+                    const char* slot = stage_begin();
+                    f32x16 acc = (f32x16){};
+                    gemm(acc, slot, gB, gB, 1, MBt(), NK1t());
+                    mask_out(acc, nl - 2, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+                    store_rt(ly_ptr(nl - 1, 1), ly_int(nl - 1, 4), myslot, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+                } else {
+                    zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NKH; ++k) Bh[k] = Oh[k];
+        }
+        // ---- hidden dgrad chain l = nl-2 .. 1
+        for (int l = nl - 2; l >= 1; --l) {
+            const int nrt = ly_int(l, 1);
+#pragma unroll
+            for (int rt = 0; rt < NRT; ++rt) {
+                if (rt < nrt) {
+                    const char* slot = stage_begin();
+                    f32x16 acc = (f32x16){};
+                    gemm(acc, slot, Bh, Bh, NKH, MBt(), NKHt());
+                    mask_out(acc, l - 1, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+                    store_rt(ly_ptr(l, 1), ly_int(l, 4), myslot, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+                } else {
+                    zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NKH; ++k) Bh[k] = Oh[k];
+        }
+        // ---- layer-0 dgrad + posenc adjoint: row (tile t, register r) = slot 16 t + r of the
+        //      lane's coordinate: slot 2k = sin band k, 2k + 1 = cos band k, 2L = the raw coordinate
+        float dc = 0.f;
+        {
+            const int nta = a.nta;
+#pragma unroll
+            for (int t = 0; t < C::NTA; ++t) {
+                if (t < nta) {
+                    const char* slot = stage_begin();
+                    f32x16 acc = (f32x16){};
+                    gemm(acc, slot, Bh, Bh, NKH, MBt(), NKHt());
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int k = 8 * t + i;
+                        if (k < L) {
+                            float s, co;
+                            band_sincos<true>(cd, k, s, co);
+                            float gs = acc[2 * i], gc = acc[2 * i + 1];
+                            if (a.c2f_on) {
+                                const float w = c2f_l[k];
+                                gs = gs * w;
+                                gc = gc * w;
+                            }
+                            dc += (gs * co - gc * s) * ldexpf(pi_f, k);
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        if (16 * t + r == 2 * L) dc += acc[r];
+                    if (t + 1 < nta) dummies(STt());
+                }
+            }
+        }
+        // (u, v) = X[:2] / (X[2] + 1e-8) backward, then the bmm backward -> dH partial of the wave
+        {
+            const float dother = __shfl_xor(dc, 32, 64);
+            const float du = h ? dother : dc, dv = h ? dc : dother;
+            float h9[9];
+#pragma unroll
+            for (int e = 0; e < 9; ++e) h9[e] = 0.f;
+            if (h == 0 && valid) {
+                const float dd = X[2] + 1e-8f;
+                const float dX0 = du / dd, dX1 = dv / dd;
+                const float dd2 = dd * dd;
+                const float dX2 = (-du * X[0]) / dd2 + (-dv * X[1]) / dd2;
+                const float hom[3] = {x, y, 1.f};
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) {
+                    h9[0 + cc] = dX0 * hom[cc];
+                    h9[3 + cc] = dX1 * hom[cc];
+                    h9[6 + cc] = dX2 * hom[cc];
+                }
+            }
+            float mine = 0.f;
+#pragma unroll
+            for (int e = 0; e < 9; ++e) {
+                const float s = wave_total63(h9[e]);
+                const float sb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 63));
+                if (lane == e) mine = sb;
+            }
+            float* dst = lane < 9 ? a.dH_partial + (size_t)(slot0 / 32) * 9 + lane : dmy;
+            s2_st4(dst, mine);
+            dummies(ST1t());
+        }
+    }
+
+    // ---- per-block partials (fixed order over waves)
+    s2_wait_vm<0>();
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(smem);  // the ring is idle now
+    {
+        const double s0 = wave_total63(lsq), s1 = wave_total63(lms);
+        const float t0 = wave_total63(bl0), t1 = wave_total63(bl1), t2 = wave_total63(bl2);
+        if (lane == 63) {
+            red[wave * 5 + 0] = s0;
+            red[wave * 5 + 1] = s1;
+            red[wave * 5 + 2] = (double)t0;
+            red[wave * 5 + 3] = (double)t1;
+            red[wave * 5 + 4] = (double)t2;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        double s = 0.0;
+        float sf = 0.f;
+        for (int w = 0; w < NW; ++w) {
+            s += red[w * 5 + threadIdx.x];
+            sf += (float)red[w * 5 + threadIdx.x];
+        }
+        if (threadIdx.x < 2) a.loss_partial[2 * (size_t)blockIdx.x + threadIdx.x] = s;
+        else a.blast_partial[3 * (size_t)blockIdx.x + threadIdx.x - 2] = sf;
+    }
+    for (int e = threadIdx.x; e < 3 * a.Kl; e += NW * 64) {
+        float s = 0.f;
+        for (int w = 0; w < NW; ++w)
+            s += reinterpret_cast<const float*>(smem + a.lds_wave + w * a.lds_wave_bytes + 2048 + MAXR * C::NMW * 256)[e];
+        a.wlast_partial[(size_t)blockIdx.x * 3 * a.Kl + e] = s;
+    }
+}
+
+// ------------------------------------------------------------------ weight program packing
+
+// true input feature of layer-0 forward k index (16 ks + 8 h + j) in the band-group layout; -1: zero
+MARF_DEV int s2_l0_fwd_feature(int ks, int hh, int j, int L, int nk0) {
+    const int ng = nk0 - 1;
+    if (ks == ng) return j == 0 ? hh : -1;  // raw coordinate
+    const int k = 4 * ks + (j & 3);
+    if (k >= L) return -1;
+    const bool cosp = j >= 4;
+    return 2 + 2 * hh * L + (cosp ? L : 0) + k;
+}
+// true input feature of adjoint row rho of tile t (slot 16 t + r of coordinate hh); -1: none
+MARF_DEV int s2_l0_adj_feature(int t, int rho, int L) {
+    const int hh = (rho >> 2) & 1, r = (rho & 3) + 4 * (rho >> 3);
+    const int sl = 16 * t + r;
+    if (sl == 2 * L) return hh;
+    if (sl >= 2 * L) return -1;
+    const int k = sl >> 1;
+    return 2 + 2 * hh * L + ((sl & 1) ? L : 0) + k;
+}
+// permuted k (hidden operand from an accumulator): k-step ks, lane half hh, element j
+MARF_DEV int s2_kperm(int ks, int hh, int j) { return 16 * ks + 8 * (j >> 2) + 4 * hh + (j & 3); }
+
+// One thread per (stage, part, k-step, lane, element): the packed bf16 value.  Stage sequence per
+// pixel tile (the kernel's consumption order): layer-0 forward row tiles, hidden forward row tiles,
+// the last layer, last-layer dgrad row tiles, hidden dgrad row tiles (l = nl-2 .. 1), adjoint tiles.
+__global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog, float* __restrict__ bias_out,
+                        int* __restrict__ kmap, Pack2Args a) {
+    const int per_slot = a.slot_bytes / 2;
+    const long long total = (long long)a.n_stages * per_slot;
+    const int D = a.dims[0];
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total + a.nbias + D; e += (long long)gridDim.x * 256) {
+        if (e >= total + a.nbias) {
+            // layer-0 column map: true input feature f -> column of feat_0 (16 ks + 8 h + j)
+            const int f = (int)(e - total - a.nbias), L = a.L, ng = a.nk0 - 1;
+            int col;
+            if (f < 2) col = 16 * ng + 8 * f;
+            else {
+                const int q = f - 2, hh = q / (2 * L), rr = q - hh * 2 * L, cosp = rr >= L, k = rr - cosp * L;
+                col = 16 * (k / 4) + 8 * hh + 4 * cosp + (k % 4);
+            }
+            kmap[f] = col;
+            continue;
+        }
+        if (e >= total) {
+            // padded bias table
+            const int be = (int)(e - total);
+            float v = 0.f;
+            for (int l = 0; l < a.nl; ++l) {
+                const int nb = (l == a.nl - 1) ? 32 : a.Mp[l];
+                if (be >= a.boff[l] && be < a.boff[l] + nb) {
+                    const int m = be - a.boff[l];
+                    if (m < a.dims[l + 1]) v = params[a.b_off[l] + m];
+                }
+            }
+            bias_out[be] = v;
+            continue;
+        }
+        int st = (int)(e / per_slot);
+        const int w = (int)(e - (long long)st * per_slot);
+        const int part = w / (a.NKH * 512);  // 0 hi, 1 lo
+        const int w2 = w - part * a.NKH * 512;
+        const int ks = w2 / 512, lane = (w2 >> 3) & 63, j = w2 & 7;
+        const int r32 = lane & 31, hh = lane >> 5;
+        float val = 0.f;
+        bool have = false;
+        // decode the stage
+        int layer = -1, kind = -1, rt = 0;  // kind 0 fwd, 1 last fwd, 2 last dgrad, 3 hidden dgrad, 4 adjoint
+        {
+            int s = st;
+            if (s < a.nrt[0]) { layer = 0; kind = 0; rt = s; }
+            else {
+                s -= a.nrt[0];
+                for (int l = 1; l < a.nl - 1 && kind < 0; ++l) {
+                    if (s < a.nrt[l]) { layer = l; kind = 0; rt = s; }
+                    else s -= a.nrt[l];
+                }
+                if (kind < 0) {
+                    if (s == 0) { layer = a.nl - 1; kind = 1; rt = 0; }
+                    else {
+                        s -= 1;
+                        if (s < a.nrtb[a.nl - 1]) { layer = a.nl - 1; kind = 2; rt = s; }
+                        else {
+                            s -= a.nrtb[a.nl - 1];
+                            for (int l = a.nl - 2; l >= 1 && kind < 0; --l) {
+                                if (s < a.nrtb[l]) { layer = l; kind = 3; rt = s; }
+                                else s -= a.nrtb[l];
+                            }
+                            if (kind < 0 && s < a.nta) { layer = 0; kind = 4; rt = s; }
+                        }
+                    }
+                }
+            }
+        }
+        if (kind >= 0) {
+            const int Mt = a.dims[layer + 1], Kt = a.dims[layer];
+            const float* W = params + a.w_off[layer];
+            int m = -1, k = -1;  // W[m][k]
+            if (kind == 0 && layer == 0) {
+                if (ks < a.nk0) {
+                    m = 32 * rt + r32;
+                    k = s2_l0_fwd_feature(ks, hh, j, a.L, a.nk0);
+                }
+            } else if (kind == 0 || kind == 1) {
+                m = 32 * rt + r32;
+                k = s2_kperm(ks, hh, j);
+            } else if (kind == 2) {
+                // rows = input features of the last layer (natural), k = [g hi (3), 0, g lo (3), 0]
+                if (ks == 0 && hh == 0 && (j & 3) < 3) {
+                    m = j & 3;
+                    k = 32 * rt + r32;
+                }
+            } else if (kind == 3) {
+                m = s2_kperm(ks, hh, j);
+                k = 32 * rt + r32;
+            } else {  // adjoint rows
+                m = s2_kperm(ks, hh, j);
+                k = s2_l0_adj_feature(rt, r32, a.L);
+            }
+            if (m >= 0 && k >= 0 && m < Mt && k < Kt) {
+                val = W[(size_t)m * Kt + k];
+                have = true;
+            }
+        }
+        u16 out = 0;
+        if (have) {
+            const u16 hi = f2bf(val);
+            out = part == 0 ? hi : (a.split ? f2bf(val - bf2f(hi)) : (u16)0);
+        }
+        prog[e] = out;
+    }
+}
+
+}  // namespace marf
+
+using namespace marf;
+
+template <int HM, bool SPLIT, int NW, int MAXR>
+static hipError_t launch_step2_t(const Step2Args& a, int grid, hipStream_t s) {
+    hipError_t e = ensure_dynamic_lds((const void*)k_step2<HM, SPLIT, NW, MAXR>, (size_t)a.lds_total);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_step2<HM, SPLIT, NW, MAXR>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
+    return hipGetLastError();
+}
+
+// variant: 0 = bf16 256-wide (8 waves), 1 = split 256-wide (4 waves), 2 = bf16 512-wide (4 waves)
+hipError_t marf_launch_step2(const Step2Args& a, int variant, int grid, hipStream_t s) {
+    switch (variant) {
+        case 0: return launch_step2_t<256, false, 8, 4>(a, grid, s);
+        case 1: return launch_step2_t<256, true, 4, 4>(a, grid, s);
+        case 2: return launch_step2_t<256, false, 4, 4>(a, grid, s);  // diagnostic: bf16 on 4 waves
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t marf_launch_pack2(const float* params, void* prog, float* bias_out, int* kmap, const Pack2Args& a,
+                             hipStream_t s) {
+    const long long total = (long long)a.n_stages * (a.slot_bytes / 2) + a.nbias + a.dims[0];
+    long long blocks = (total + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(k_pack2, dim3((unsigned)blocks), dim3(256), 0, s, params, (u16*)prog, bias_out, kmap, a);
+    return hipGetLastError();
+}

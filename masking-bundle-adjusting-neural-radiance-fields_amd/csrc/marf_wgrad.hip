@@ -442,7 +442,8 @@ __global__ __launch_bounds__(256) void k_wgrad_last(const float* __restrict__ gl
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ partial,
                                                       const float* __restrict__ bpartial, int n_chunks, int M, int K,
                                                       int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db,
-                                                      const float* __restrict__ gscale, const float* __restrict__ denom) {
+                                                      const float* __restrict__ gscale, const float* __restrict__ denom,
+                                                      const int* __restrict__ kmap) {
     __shared__ float red[4][64];
     const long long n = (long long)Mo * Ko;
     const long long e = blockIdx.x * 64LL + (threadIdx.x & 63);
@@ -454,7 +455,8 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
         size_t stride;
         if (e < n) {
             const int m = (int)(e / Ko), k = (int)(e % Ko);
-            src = partial + (size_t)m * K + k;
+            // kmap: column of true input feature k in the partial (the step2 layer-0 layout)
+            src = partial + (size_t)m * K + (kmap ? kmap[k] : k);
             stride = (size_t)M * K;
         } else {
             src = bpartial + (e - n);
@@ -607,7 +609,7 @@ hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* fea
 
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
                                     int Ko, float* dW, float* db, hipStream_t s, const float* gscale,
-                                    const float* denom, float* scratch) {
+                                    const float* denom, float* scratch, const int* kmap) {
     if (n_chunks > 1024 && scratch) {
         // fold into G <= 256 groups first (n_chunks up to millions of partials)
         const int per = (n_chunks + 255) / 256;
@@ -626,6 +628,6 @@ hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial,
     long long n = (long long)Mo * Ko + Mo;
     int blocks = (int)((n + 63) / 64);
     hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, s, partial, bpartial, n_chunks, M, K, Mo, Ko, dW, db,
-                       gscale, denom);
+                       gscale, denom, kmap);
     return hipGetLastError();
 }

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MARF_LIB selects a diagnostic build (lib/libmarf_stamps.so, tools/phase_stamps.py)
 LIB_PATH = os.environ.get("MARF_LIB") or os.path.join(_HERE, "lib", "libmarf.so")
 
-MARF_FP32, MARF_BF16 = 0, 1
+MARF_FP32, MARF_BF16, MARF_BF16X3 = 0, 1, 2
 GEO_GRID, GEO_COORDS, GEO_CANVAS = 0, 1, 2
 
 _c_int, _c_ll, _c_dbl, _c_vp, _c_sz = ctypes.c_int, ctypes.c_longlong, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t

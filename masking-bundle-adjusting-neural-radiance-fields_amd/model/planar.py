@@ -35,7 +35,9 @@ def _precision(opt):
         return marf_hip.MARF_FP32
     if p in ("bf16", "bfloat16"):
         return marf_hip.MARF_BF16
-    raise ValueError(f"precision must be fp32 or bf16, got {p}")
+    if p in ("bf16x3", "split-bf16"):
+        return marf_hip.MARF_BF16X3
+    raise ValueError(f"precision must be fp32, bf16 or bf16x3, got {p}")
 
 
 def _dist():
