@@ -102,7 +102,7 @@ static void plan_step2_net(marf_net* n) {
     }
     q.nbias = bo;
     for (int l = 0; l < nl - 1; ++l) st += q.nrt[l];
-    st += 1 + q.nrtb[nl - 1];
+    st += 2;  // last layer forward, last-layer dgrad (every row tile in one stage)
     for (int l = nl - 2; l >= 1; --l) st += q.nrtb[l];
     st += q.nta;
     q.n_stages = st;
@@ -747,6 +747,7 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     a.Kl = q.Kl;
     a.c2f_w = (const float*)(sv + p.c2f);
     a.dummy = (float*)(sv + p.dummy);
+    a.stamps = g_stamps;
     a.n_tiles = p.n_tiles;
     // LDS layout
     const int TPX = 32 * q.NW;

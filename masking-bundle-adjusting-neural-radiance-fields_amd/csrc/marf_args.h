@@ -100,6 +100,7 @@ struct Step2Args {
     int Kl;                          // padded input width of the last layer
     const float* c2f_w;              // [L] band weights of this step
     float* dummy;                    // [grid][NW][ST][64][2] store sink
+    unsigned long long* stamps;      // diagnostic builds (MARF_STAMPS): [grid][8] cycle totals of wave 0
     int n_tiles;                     // block tiles of 32 * NW pixel slots
     // LDS layout (byte offsets; computed on the host)
     int lds_pro, lds_bias, lds_c2f, lds_layers, lds_wave, lds_wave_bytes, lds_total;

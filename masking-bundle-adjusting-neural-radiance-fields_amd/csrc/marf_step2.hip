@@ -79,6 +79,16 @@ MARF_DEV i16x4 s2_tr16(const u16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
 }
 
+// compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1
+template <int... I, class F>
+MARF_DEV void s2_sfor_impl(std::integer_sequence<int, I...>, F&& f) {
+    (f(std::integral_constant<int, I>()), ...);
+}
+template <int N, class F>
+MARF_DEV void s2_sfor(F&& f) {
+    s2_sfor_impl(std::make_integer_sequence<int, N>(), f);
+}
+
 // two floats -> packed bf16 pair (v_cvt_pk_bf16_f32, RNE)
 MARF_DEV uint32_t s2_pk(float a, float b) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -110,6 +120,20 @@ MARF_DEV void s2_split8(const float* x, S2Frag& hi, S2Frag& lo) {
 }
 
 // ------------------------------------------------------------------ the kernel
+
+// Diagnostic phase timing (MARF_STAMPS builds): wave 0 of each block sums s_memtime deltas per
+// phase category; tools/step2_phases.py reads them.
+#ifdef MARF_STAMPS
+#define S2T_BEGIN(k) const unsigned long long _t##k = __builtin_amdgcn_s_memtime()
+#define S2T_END(k) tacc[k] += __builtin_amdgcn_s_memtime() - _t##k
+#else
+#define S2T_BEGIN(k) \
+    do {         \
+    } while (0)
+#define S2T_END(k) \
+    do {       \
+    } while (0)
+#endif
 
 template <int HM, bool SPLIT, int NW, int MAXR>
 struct S2Cfg {
@@ -156,6 +180,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     uint32_t* mkl = reinterpret_cast<uint32_t*>(wpriv + 2048);  // ReLU mask words [MAXR][NMW][64]
     float* wla = reinterpret_cast<float*>(wpriv + 2048 + MAXR * C::NMW * 256);  // [3][Kl] dW_last
     float* dmy = a.dummy + (((size_t)blockIdx.x * NW + wave) * ST * 64 + lane) * 2;
+#ifdef MARF_STAMPS
+    unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
     // ---- constants into LDS (plain loads: the compiler's waits are harmless before the ring)
     for (int e = threadIdx.x; e < a.nbias; e += NW * 64) bias_l[e] = a.bias[e];
@@ -203,14 +230,43 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         ++dma_stage;
         if (++dma_prog == a.n_stages) dma_prog = 0;
     };
+    // The refill of the slot freed at a stage's barrier is issued piece by piece beside the stage's
+    // MFMAs (dma_piece from the GEMM loop), the rest before the stage's first store (dma_flush):
+    // LDS-DMA issue is throttled by the CU's L2 -> LDS rate, so a burst would stall the wave.
+    int dma_left = 0;
+    unsigned dma_dst = 0;
+    const char* dma_src = nullptr;
+    auto dma_arm = [&]() {
+        dma_dst = lds0 + (dma_stage % C::NSLOT) * C::SLOT + wave * C::PER_DMA * 1024;
+        dma_src = a.prog + (size_t)dma_prog * C::SLOT + wave * C::PER_DMA * 1024 + lane * 16;
+        dma_left = C::PER_DMA;
+        ++dma_stage;
+        if (++dma_prog == a.n_stages) dma_prog = 0;
+    };
+    auto dma_piece = [&]() {
+        if (dma_left > 0) {
+            s2_glds16(dma_src, __builtin_amdgcn_readfirstlane(dma_dst));
+            dma_src += 1024;
+            dma_dst += 1024;
+            --dma_left;
+        }
+    };
+    auto dma_flush = [&]() {
+        while (dma_left > 0) dma_piece();
+    };
     // wait for stage c_stage, publish it to every wave, refill the slot freed by stage c_stage - 1
     auto stage_begin = [&]() -> const char* {
+        dma_flush();
+        S2T_BEGIN(0);
         if (c_stage + 1 < total) s2_wait_vm<C::D * ST + C::PER_DMA>();
         else s2_wait_vm<C::D * ST>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (dma_stage < total) issue_stage();
+        S2T_END(0);
+        S2T_BEGIN(1);
+        if (dma_stage < total) dma_arm();
+        S2T_END(1);
         const char* slot = smem + (c_stage % C::NSLOT) * C::SLOT;
         ++c_stage;
         return slot;
@@ -237,6 +293,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
 
     auto dummies = [&](auto n_tag) {
         constexpr int N = decltype(n_tag)::value;
+        dma_flush();
 #pragma unroll
         for (int i = 0; i < N; ++i) s2_st8(dmy + i * 128, 0u, 0u);
     };
@@ -245,6 +302,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     // (the stores of a row tile into a natural-order [S][ld] bf16 tensor: k-step ks of the lane's
     //  pixel holds columns 16 ks + 4 h + 0..3 (elements 0-3) and 16 ks + 8 + 4 h + 0..3 (4-7))
     auto store_rt = [&](u16* base, int ld, long long slot, int rt, const S2Frag& f0, const S2Frag& f1) {
+        dma_flush();
         u16* row = base + slot * ld;
         s2_st8(row + 32 * rt + 4 * h, f0.u.x, f0.u.y);
         s2_st8(row + 32 * rt + 8 + 4 * h, f0.u.z, f0.u.w);
@@ -254,14 +312,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
 
     // one 32-row output tile: acc (+)= A[ks] . B[ks] over NK k-steps from the slot
     //   MODE 0: plain; 1: split forward (hi.hi + hi.lo + lo.hi); 2: split dgrad (hi.B + lo.B)
+    auto nohook = [&](auto) {};
     auto gemm = [&](f32x16& acc, const char* slot, const S2Frag* Bhi, const S2Frag* Blo, int nk, auto mode_tag,
-                    auto nk_tag) {
+                    auto nk_tag, auto&& hook) {
         constexpr int MODE = decltype(mode_tag)::value;
         constexpr int NK = decltype(nk_tag)::value;
         const bf16x8* ah = reinterpret_cast<const bf16x8*>(slot + lane * 16);
         const bf16x8* al = reinterpret_cast<const bf16x8*>(slot + C::LO + lane * 16);
         // 4-deep register ring of A fragments; sched_barrier pins the issue order (left alone the
-        // scheduler sinks each LDS read to right before its MFMA and exposes its latency)
+        // scheduler sinks each LDS read to right before its MFMA and exposes its latency).  hook(ks)
+        // is VALU work of the previous row tile's epilogue, placed beside the MFMAs of step ks.
         constexpr int P = NK < 4 ? NK : 4;
         bf16x8 A0[4], A1[4];
 #pragma unroll
@@ -269,10 +329,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             A0[u] = ah[u * 64];
             if constexpr (MODE != 0) A1[u] = al[u * 64];
         }
-#pragma unroll
-        for (int ks = 0; ks < NK; ++ks) {
+        s2_sfor<NK>([&](auto ksc) {
+            constexpr int ks = decltype(ksc)::value;
+            constexpr int u = ks & 3;
             const bool live = NK != C::NK0 || ks < nk;
-            const int u = ks & 3;
             __builtin_amdgcn_sched_barrier(0);
             if (live) {
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0[u], Bhi[ks].f, acc, 0, 0, 0);
@@ -282,13 +342,19 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 } else if constexpr (MODE == 2) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[u], Bhi[ks].f, acc, 0, 0, 0);
                 }
+                hook(ksc);
+                if constexpr (NK >= 2 * C::PER_DMA) {
+                    if constexpr ((ks & 1) == 1) dma_piece();
+                } else {
+                    dma_piece();
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
-            if (ks + P < NK) {
+            if constexpr (ks + P < NK) {
                 A0[u] = ah[(ks + P) * 64];
                 if constexpr (MODE != 0) A1[u] = al[(ks + P) * 64];
             }
-        }
+        });
     };
     typedef std::integral_constant<int, 0> M0t;
     typedef std::integral_constant<int, SPLIT ? 1 : 0> MFt;
@@ -350,15 +416,74 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         s2_split8<false>(v + 8, o1, dumm);
     };
 
+    // pipelined epilogues: micro-steps of one 32-row accumulator tile
+    long long myslot_g = 0;
+    struct EpSt {
+        uint32_t bits, mw;
+        float vp;
+        uint32_t hw[8], lw[8];
+    } ep;
+    f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
+    // forward step e: ReLU + mask bit of register e; the odd steps pack the (hi, lo) bf16 pair
+    auto fstep = [&](const f32x16& pa, auto ec) {
+        constexpr int e = decltype(ec)::value;
+        float x;
+        asm volatile(
+            "v_cmp_lt_f32_e32 vcc, 0, %2\n\t"
+            "v_cndmask_b32_e32 %0, 0, %2, vcc\n\t"
+            "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+            : "=&v"(x), "+v"(ep.bits)
+            : "v"(pa[e])
+            : "vcc");
+        if constexpr (e & 1) {
+            const uint32_t w = s2_pk(ep.vp, x);
+            ep.hw[e >> 1] = w;
+            if constexpr (SPLIT) ep.lw[e >> 1] = s2_pk(ep.vp - s2_lo16(w), x - s2_hi16(w));
+        } else {
+            ep.vp = x;
+        }
+    };
+    // forward finish of tile rt: operand fragments of k-steps 2 rt, 2 rt + 1, mask word, 4 stores
+    auto ffinish = [&](int l, auto rtc, bool save, u16* sbase, int sld) {
+        constexpr int rt = decltype(rtc)::value;
+        Oh[2 * rt].u = make_uint4(ep.hw[0], ep.hw[1], ep.hw[2], ep.hw[3]);
+        Oh[2 * rt + 1].u = make_uint4(ep.hw[4], ep.hw[5], ep.hw[6], ep.hw[7]);
+        if constexpr (SPLIT) {
+            Ol[2 * rt].u = make_uint4(ep.lw[0], ep.lw[1], ep.lw[2], ep.lw[3]);
+            Ol[2 * rt + 1].u = make_uint4(ep.lw[4], ep.lw[5], ep.lw[6], ep.lw[7]);
+        }
+        if constexpr ((rt & 1) == 0) mpend = ep.bits << 16;
+        else mkl[(l * C::NMW + (rt >> 1)) * 64 + lane] = mpend | ep.bits;
+        if (save) store_rt(sbase, sld, myslot_g, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+        else dummies(std::integral_constant<int, ST>());
+    };
+    // dgrad step e: dz = acc * relu'(z) with the mask word ep.mw
+    auto bstep = [&](const f32x16& pa, auto ec, auto rtc) {
+        constexpr int e = decltype(ec)::value;
+        constexpr int rt = decltype(rtc)::value;
+        const int m = __builtin_amdgcn_sbfe((int)ep.mw, 16 * (1 - (rt & 1)) + 15 - e, 1);
+        const float x = __int_as_float(__float_as_int(pa[e]) & m);
+        if constexpr (e & 1) ep.hw[e >> 1] = s2_pk(ep.vp, x);
+        else ep.vp = x;
+    };
+    auto bfinish = [&](auto rtc, u16* sbase, int sld) {
+        constexpr int rt = decltype(rtc)::value;
+        Oh[2 * rt].u = make_uint4(ep.hw[0], ep.hw[1], ep.hw[2], ep.hw[3]);
+        Oh[2 * rt + 1].u = make_uint4(ep.hw[4], ep.hw[5], ep.hw[6], ep.hw[7]);
+        store_rt(sbase, sld, myslot_g, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+    };
     const float pi_f = 3.14159265358979323846f;
 
+    S2T_BEGIN(7);
     for (int it = 0; it < my_tiles; ++it) {
+        S2T_BEGIN(4);
         const int tile = (int)blockIdx.x + it * (int)gridDim.x;
         const int pb = it & 1;
         const int b = tile / tpp;
         const int p0 = (tile - b * tpp) * C::TPX + 32 * wave;
         const long long slot0 = (long long)b * a.geo.Np_pad + p0;
         const long long myslot = slot0 + pxl;
+        myslot_g = myslot;
         const int p = p0 + pxl;
         const bool valid = p < Np;
         const float* pro = pro_buf(pb);
@@ -417,62 +542,70 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             if (16 * a.nk0 < ly_int(0, 3)) s2_st16(row + 16 * a.nk0 + 8 * h, make_uint4(0, 0, 0, 0));
         }
 
-        // ---- layer 0 forward
-        {
-            const int nrt = ly_int(0, 0);
-            const bool save = nl > 2;
-#pragma unroll
-            for (int rt = 0; rt < NRT; ++rt) {
+        S2T_END(4);
+        S2T_BEGIN(5);
+        // ---- forward, layer 0 then the hidden layers: one stage per 32-row output tile; the
+        //      epilogue of tile rt-1 (ReLU, mask bits, bf16 split, stores) runs beside the MFMAs
+        //      of tile rt, the last tile's epilogue right after its own MFMAs
+        auto fwd_layer = [&](int l, const S2Frag* Bhi, const S2Frag* Blo, int nk, auto nk_tag, auto ms_tag) {
+            constexpr int MS = decltype(ms_tag)::value;  // epilogue micro-steps beside each k-step
+            const int nrt = ly_int(l, 0);
+            const bool save = l + 1 < nl - 1;
+            u16* sbase = save ? ly_ptr(l + 1, 0) : nullptr;
+            const int sld = save ? ly_int(l + 1, 3) : 0;
+            const int boff = ly_int(l, 2);
+            s2_sfor<NRT>([&](auto rtc) {
+                constexpr int rt = decltype(rtc)::value;
+                f32x16& cur = (rt & 1) ? acc1 : acc0;
+                f32x16& prv = (rt & 1) ? acc0 : acc1;
                 if (rt < nrt) {
                     const char* slot = stage_begin();
                     // the next tile's target / mask / H into the other input buffer (the tile that
                     // read it last finished before this stage's barrier)
-                    if (rt == 0 && it + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
-                    f32x16 acc = bias_init(ly_int(0, 2), rt);
-                    gemm(acc, slot, F0h, F0l, a.nk0, MFt(), NK0t());
-                    relu_out(acc, 0, rt, Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
-                    if (save) store_rt(ly_ptr(1, 0), ly_int(1, 3), myslot, rt, Oh[2 * rt], Oh[2 * rt + 1]);
-                    else dummies(STt());
+                    if (l == 0 && rt == 0 && it + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
+                    cur = bias_init(boff, rt);
+                    if constexpr (rt == 0) {
+                        gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, nohook);
+                        dummies(STt());
+                    } else {
+                        ep.bits = 0;
+                        gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, [&](auto ksc) {
+                            s2_sfor<MS>([&](auto jc) {
+                                constexpr int e = decltype(ksc)::value * MS + decltype(jc)::value;
+                                if constexpr (e < 16) fstep(prv, std::integral_constant<int, e>());
+                            });
+                        });
+                        s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
+                            if (decltype(ec)::value >= MS * nk) fstep(prv, ec);
+                        });
+                        ffinish(l, std::integral_constant<int, rt - 1>(), save, sbase, sld);
+                    }
+                    if (rt == nrt - 1) {
+                        ep.bits = 0;
+                        s2_sfor<16>([&](auto ec) { fstep(cur, ec); });
+                        ffinish(l, rtc, save, sbase, sld);
+                    }
                 } else {
                     zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
                 }
-            }
+            });
 #pragma unroll
             for (int k = 0; k < NKH; ++k) {
                 Bh[k] = Oh[k];
                 if constexpr (SPLIT) Bl[k] = Ol[k];
             }
-        }
-        // ---- hidden layers forward
-        for (int l = 1; l < nl - 1; ++l) {
-            const int nrt = ly_int(l, 0);
-            const bool save = l + 1 < nl - 1;
-#pragma unroll
-            for (int rt = 0; rt < NRT; ++rt) {
-                if (rt < nrt) {
-                    const char* slot = stage_begin();
-                    f32x16 acc = bias_init(ly_int(l, 2), rt);
-                    gemm(acc, slot, Bh, Bl, NKH, MFt(), NKHt());
-                    relu_out(acc, l, rt, Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
-                    if (save) store_rt(ly_ptr(l + 1, 0), ly_int(l + 1, 3), myslot, rt, Oh[2 * rt], Oh[2 * rt + 1]);
-                    else dummies(STt());
-                } else {
-                    zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < NKH; ++k) {
-                Bh[k] = Oh[k];
-                if constexpr (SPLIT) Bl[k] = Ol[k];
-            }
-        }
+        };
+        fwd_layer(0, F0h, F0l, a.nk0, NK0t(), std::integral_constant<int, 2>());
+        for (int l = 1; l < nl - 1; ++l) fwd_layer(l, Bh, Bl, NKH, NKHt(), std::integral_constant<int, 1>());
 
+        S2T_END(5);
+        S2T_BEGIN(6);
         // ---- last layer: 3 outputs (rows 0..2 of one tile), sigmoid, masked MSE, d rgb
         float g[3] = {0.f, 0.f, 0.f};
         {
             const char* slot = stage_begin();
             f32x16 acc = bias_init(ly_int(nl - 1, 2), 0);
-            gemm(acc, slot, Bh, Bl, NKH, MFt(), NKHt());
+            gemm(acc, slot, Bh, Bl, NKH, MFt(), NKHt(), nohook);
             float* o = (a.rgb && valid && h == 0) ? a.rgb + ((size_t)b * Np + p) * 3 : dmy;
             float yv[3] = {0.f, 0.f, 0.f};
             if (h == 0) {
@@ -498,6 +631,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 bl1 += g[1];
                 bl2 += g[2];
             }
+            dma_flush();
             s2_st12(o, yv[0], yv[1], yv[2]);
             dummies(ST1t());
         }
@@ -549,76 +683,132 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             }
         }
 
-        // ---- last-layer dgrad: dfeat_{n-1} = W_{n-1}^T g, mask -> dz_{n-1}
+        S2T_END(6);
+        S2T_BEGIN(2);
+        // ---- last-layer dgrad: dfeat_{n-1} = W_{n-1}^T g, mask -> dz_{n-1}; one stage holds every
+        //      row tile's single k-step (tile rt at rt KB), epilogues pipelined across the tiles
         {
+            const int lmask = nl - 2;
             const int nrt = ly_int(nl - 1, 1);
+            u16* sbase = ly_ptr(nl - 1, 1);
+            const int sld = ly_int(nl - 1, 4);
             S2Frag gB[1] = {Bg};
-#pragma unroll
-            for (int rt = 0; rt < NRT; ++rt) {
+            const char* slot = stage_begin();
+            s2_sfor<NRT>([&](auto rtc) {
+                constexpr int rt = decltype(rtc)::value;
+                f32x16& cur = (rt & 1) ? acc1 : acc0;
+                f32x16& prv = (rt & 1) ? acc0 : acc1;
                 if (rt < nrt) {
-                    const char* slot = stage_begin();
-                    f32x16 acc = (f32x16){};
-                    gemm(acc, slot, gB, gB, 1, MBt(), NK1t());
-                    mask_out(acc, nl - 2, rt, Oh[2 * rt], Oh[2 * rt + 1]);
-                    store_rt(ly_ptr(nl - 1, 1), ly_int(nl - 1, 4), myslot, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+                    cur = (f32x16){};
+                    if constexpr (rt == 0) {
+                        gemm(cur, slot, gB, gB, 1, MBt(), NK1t(), nohook);
+                    } else {
+                        ep.mw = mkl[(lmask * C::NMW + ((rt - 1) >> 1)) * 64 + lane];
+                        gemm(cur, slot + rt * 1024, gB, gB, 1, MBt(), NK1t(), [&](auto) {
+                            s2_sfor<16>([&](auto ec) { bstep(prv, ec, std::integral_constant<int, rt - 1>()); });
+                        });
+                        bfinish(std::integral_constant<int, rt - 1>(), sbase, sld);
+                    }
+                    if (rt == nrt - 1) {
+                        ep.mw = mkl[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
+                        s2_sfor<16>([&](auto ec) { bstep(cur, ec, rtc); });
+                        bfinish(rtc, sbase, sld);
+                    }
                 } else {
                     zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
                 }
-            }
+            });
 #pragma unroll
             for (int k = 0; k < NKH; ++k) Bh[k] = Oh[k];
         }
         // ---- hidden dgrad chain l = nl-2 .. 1
         for (int l = nl - 2; l >= 1; --l) {
+            const int lmask = l - 1;
             const int nrt = ly_int(l, 1);
-#pragma unroll
-            for (int rt = 0; rt < NRT; ++rt) {
+            u16* sbase = ly_ptr(l, 1);
+            const int sld = ly_int(l, 4);
+            s2_sfor<NRT>([&](auto rtc) {
+                constexpr int rt = decltype(rtc)::value;
+                f32x16& cur = (rt & 1) ? acc1 : acc0;
+                f32x16& prv = (rt & 1) ? acc0 : acc1;
                 if (rt < nrt) {
                     const char* slot = stage_begin();
-                    f32x16 acc = (f32x16){};
-                    gemm(acc, slot, Bh, Bh, NKH, MBt(), NKHt());
-                    mask_out(acc, l - 1, rt, Oh[2 * rt], Oh[2 * rt + 1]);
-                    store_rt(ly_ptr(l, 1), ly_int(l, 4), myslot, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+                    cur = (f32x16){};
+                    if constexpr (rt == 0) {
+                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), nohook);
+                        dummies(STt());
+                    } else {
+                        ep.mw = mkl[(lmask * C::NMW + ((rt - 1) >> 1)) * 64 + lane];
+                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), [&](auto ksc) {
+                            bstep(prv, ksc, std::integral_constant<int, rt - 1>());
+                        });
+                        bfinish(std::integral_constant<int, rt - 1>(), sbase, sld);
+                    }
+                    if (rt == nrt - 1) {
+                        ep.mw = mkl[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
+                        s2_sfor<16>([&](auto ec) { bstep(cur, ec, rtc); });
+                        bfinish(rtc, sbase, sld);
+                    }
                 } else {
                     zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
                 }
-            }
+            });
 #pragma unroll
             for (int k = 0; k < NKH; ++k) Bh[k] = Oh[k];
         }
         // ---- layer-0 dgrad + posenc adjoint: row (tile t, register r) = slot 16 t + r of the
-        //      lane's coordinate: slot 2k = sin band k, 2k + 1 = cos band k, 2L = the raw coordinate
+        //      lane's coordinate: slot 2k = sin band k, 2k + 1 = cos band k, 2L = the raw coordinate.
+        //      The adjoint of tile t-1 (8 bands) runs beside the MFMAs of tile t.
         float dc = 0.f;
         {
             const int nta = a.nta;
+            auto adj_band = [&](const f32x16& pa, int t, auto ic) {
+                constexpr int i = decltype(ic)::value;
+                const int k = 8 * t + i;
+                if (k < L) {
+                    float sn, co;
+                    band_sincos<true>(cd, k, sn, co);
+                    float gs = pa[2 * i], gc = pa[2 * i + 1];
+                    if (a.c2f_on) {
+                        const float w = c2f_l[k];
+                        gs = gs * w;
+                        gc = gc * w;
+                    }
+                    dc += (gs * co - gc * sn) * ldexpf(pi_f, k);
+                }
+            };
+            auto adj_raw = [&](const f32x16& pa, int t) {
 #pragma unroll
-            for (int t = 0; t < C::NTA; ++t) {
+                for (int r = 0; r < 16; ++r)
+                    if (16 * t + r == 2 * L) dc += pa[r];
+            };
+            s2_sfor<C::NTA>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                f32x16& cur = (t & 1) ? acc1 : acc0;
+                f32x16& prv = (t & 1) ? acc0 : acc1;
                 if (t < nta) {
                     const char* slot = stage_begin();
-                    f32x16 acc = (f32x16){};
-                    gemm(acc, slot, Bh, Bh, NKH, MBt(), NKHt());
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const int k = 8 * t + i;
-                        if (k < L) {
-                            float s, co;
-                            band_sincos<true>(cd, k, s, co);
-                            float gs = acc[2 * i], gc = acc[2 * i + 1];
-                            if (a.c2f_on) {
-                                const float w = c2f_l[k];
-                                gs = gs * w;
-                                gc = gc * w;
-                            }
-                            dc += (gs * co - gc * s) * ldexpf(pi_f, k);
-                        }
+                    cur = (f32x16){};
+                    if constexpr (t == 0) {
+                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), nohook);
+                    } else {
+                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), [&](auto ksc) {
+                            constexpr int ks = decltype(ksc)::value;
+                            if constexpr ((ks & 1) == 0) adj_band(prv, t - 1, std::integral_constant<int, ks / 2>());
+                        });
+                        adj_raw(prv, t - 1);
                     }
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        if (16 * t + r == 2 * L) dc += acc[r];
-                    if (t + 1 < nta) dummies(STt());
+                    if (t == nta - 1) {
+                        s2_sfor<8>([&](auto ic) { adj_band(cur, t, ic); });
+                        adj_raw(cur, t);
+                    } else {
+                        dummies(STt());
+                    }
                 }
-            }
+            });
         }
+        S2T_END(2);
+        S2T_BEGIN(3);
         // (u, v) = X[:2] / (X[2] + 1e-8) backward, then the bmm backward -> dH partial of the wave
         {
             const float dother = __shfl_xor(dc, 32, 64);
@@ -647,10 +837,17 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 if (lane == e) mine = sb;
             }
             float* dst = lane < 9 ? a.dH_partial + (size_t)(slot0 / 32) * 9 + lane : dmy;
+            dma_flush();
             s2_st4(dst, mine);
             dummies(ST1t());
         }
+        S2T_END(3);
     }
+    S2T_END(7);
+#ifdef MARF_STAMPS
+    if (a.stamps && threadIdx.x == 0)
+        for (int k = 0; k < 8; ++k) a.stamps[(size_t)blockIdx.x * 8 + k] = tacc[k];
+#endif
 
     // ---- per-block partials (fixed order over waves)
     s2_wait_vm<0>();
@@ -767,9 +964,9 @@ __global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog
                     if (s == 0) { layer = a.nl - 1; kind = 1; rt = 0; }
                     else {
                         s -= 1;
-                        if (s < a.nrtb[a.nl - 1]) { layer = a.nl - 1; kind = 2; rt = s; }
+                        if (s == 0) { layer = a.nl - 1; kind = 2; rt = 0; }  // one stage, tile rt at rt KB
                         else {
-                            s -= a.nrtb[a.nl - 1];
+                            s -= 1;
                             for (int l = a.nl - 2; l >= 1 && kind < 0; --l) {
                                 if (s < a.nrtb[l]) { layer = l; kind = 3; rt = s; }
                                 else s -= a.nrtb[l];
@@ -793,10 +990,11 @@ __global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog
                 m = 32 * rt + r32;
                 k = s2_kperm(ks, hh, j);
             } else if (kind == 2) {
-                // rows = input features of the last layer (natural), k = [g hi (3), 0, g lo (3), 0]
-                if (ks == 0 && hh == 0 && (j & 3) < 3) {
+                // rows = input features of the last layer (natural), k = [g hi (3), 0, g lo (3), 0];
+                // fragment slot ks of the stage holds row tile ks
+                if (ks < a.nrtb[layer] && hh == 0 && (j & 3) < 3) {
                     m = j & 3;
-                    k = 32 * rt + r32;
+                    k = 32 * ks + r32;
                 }
             } else if (kind == 3) {
                 m = s2_kperm(ks, hh, j);

@@ -1,5 +1,5 @@
 set -o pipefail
-for cfg in "bf16 0 0" "bf16 1 1" "bf16x3 1 0" "bf16 1 0"; do
+for cfg in "bf16 0 0" "bf16 1 1" "bf16x3 1 0"; do
   set -- $cfg
   MARF_STEP2=$2 MARF_STEP2_NW4=$3 timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --precision $1 > gpurun_out/b_$1_$2_$3.json 2> gpurun_out/b_$1_$2_$3.err || { echo "fail $cfg"; tail -3 gpurun_out/b_$1_$2_$3.err; exit 1; }
   python -c "

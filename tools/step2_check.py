@@ -64,24 +64,16 @@ def main():
         kw = dict(B=B, L=L, layers=layers)
         f32 = run("fp32", False, geo, **kw)
         old = run("bf16", False, geo, **kw)
-        new = run("bf16", True, geo, **kw)
         spl = run("bf16x3", True, geo, **kw)
         nw4 = run("bf16", True, geo, nw4=True, **kw)
-        os.environ["MARF_STEP2_GRID"] = "100000"
-        big = run("bf16", True, geo, **kw)
         os.environ["MARF_STEP2_GRID"] = "7"
-        few = run("bf16", True, geo, **kw)
         few4 = run("bf16", True, geo, nw4=True, **kw)
         fews = run("bf16x3", True, geo, **kw)
         del os.environ["MARF_STEP2_GRID"]
         print(f"== geo {geo} B {B} L {L} layers {layers}")
-        cmp("step2 bf16 vs tile bf16", new, old)
         cmp("tile bf16 vs fp32", old, f32)
-        cmp("step2 bf16 vs fp32", new, f32)
         cmp("step2 bf16x3 vs fp32", spl, f32)
         cmp("step2 bf16 (4 waves) vs fp32", nw4, f32)
-        cmp("step2 bf16 one tile per block vs fp32", big, f32)
-        cmp("step2 bf16 grid 7 vs fp32", few, f32)
         cmp("step2 bf16 (4 waves) grid 7 vs fp32", few4, f32)
         cmp("step2 bf16x3 grid 7 vs fp32", fews, f32)
 

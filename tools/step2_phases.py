@@ -1,0 +1,55 @@
+"""Per-phase cycle split of the pixel-per-wave fused step (diagnostic build with MARF_STAMPS):
+    MARF_LIB=.../libmarf_stamps.so python tools/step2_phases.py [--precision bf16x3]
+Wave 0 of each block sums s_memtime deltas per category over its tiles; printed as the mean over
+blocks, in cycles per tile and as a share of the tile loop."""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "masking-bundle-adjusting-neural-radiance-fields_amd"))
+import bench  # noqa: E402
+
+NAMES = ["stage wait+barrier", "DMA issue", "backward (BWL..BW0)", "dH tail", "prologue", "forward (FW0..FWH)",
+         "last layer + dW_last", "tile loop total"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--precision", default="bf16x3")
+    args = ap.parse_args()
+    import marf_hip
+    from model import planar
+    from util import EasyDict as edict
+    dev = torch.device("cuda", 0)
+    opt = bench.make_opt("c3", args.precision, 64)
+    opt.device = str(dev)
+    torch.manual_seed(3)
+    m = planar.Model(opt)
+    rgb, mask, warp = bench.synthetic_inputs(64, 256, 256, dev)
+    m.images = edict(rgb=rgb, masks=mask, masks_eroded=mask, edges=None, gt_hom=None, gt=None)
+    m.build_networks()
+    m.graph.warp_param.weight.data.copy_(warp)
+    m.graph.neural_image.progress.data.fill_(0.2)
+    m.graph.need_edges = False
+    var = edict(images=m.images)
+    stamps = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
+    marf_hip.lib().marf_debug_set_stamps(marf_hip._ptr(stamps))
+    for _ in range(3):
+        v = m.graph.forward(var)
+        m.graph.compute_loss(v).rgb.backward()
+    torch.cuda.synchronize()
+    st = stamps.view(-1, 8).cpu().numpy().astype(np.float64)
+    st = st[st[:, 7] > 0]
+    tiles = 4194304 // (32 * (4 if args.precision == "bf16x3" else 8)) / len(st)
+    mean = st.mean(0) / tiles
+    for n, v in zip(NAMES, mean):
+        print(f"{n:24s} {v:10.0f} cycles/tile  {100 * v / mean[7]:5.1f} %")
+
+
+if __name__ == "__main__":
+    main()
