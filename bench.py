@@ -1,6 +1,6 @@
 """Throughput of the planar bundle-adjustment training step on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c1|c5] [--precision bf16|fp32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c1|c5] [--precision bf16x3|bf16|fp32]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -8,8 +8,10 @@ A step is one full Model.train_iteration of the product (model/planar.py): fused
 grid->warp->posenc->MLP forward, masked MSE, backward (dgrad chain, warp adjoint, weight
 gradients), the RCCL all-reduce of the MLP gradient (N > 1), Adam, progress update, fix_first.
 Workload (BASELINE.json configs[2]): per GPU 64 patches of 256x256 pixels cropped
-from a 512x512 canvas, L=16 posenc, MLP 66-256-256-256-256-3, bf16 MFMA, c2f [0,0.4] at
-progress 0.2.  Synthetic targets (smooth procedural RGB, seed 0), Bernoulli(0.85) masks (seed 1),
+from a 512x512 canvas, L=16 posenc, MLP 66-256-256-256-256-3, c2f [0,0.4] at progress 0.2, in
+the precision recipe that carries the seed-3 end-to-end contract: bf16x3 (split-bf16 hi+lo MFMA
+operands with fp32 accumulation: forward hi*hi+hi*lo+lo*hi, dgrad W_hi^T dz + W_lo^T dz; DESIGN.md
+§4).  --precision bf16 (plain bf16 MFMA) and fp32 are the other recipes.  Synthetic targets (smooth procedural RGB, seed 0), Bernoulli(0.85) masks (seed 1),
 warps ~ N(0, 0.01^2) (seed 2, patch 0 fixed).  Weak scaling: 64 patches per GPU at every N.
 
 Prints one JSON line (rank 0).  `value` = pixels processed by all ranks per second.
@@ -31,6 +33,8 @@ METRIC = "warped+encoded+MLP pixels/s/GPU; final PSNR vs ref (seed=3)"
 PEAK_BF16 = 2.5e15   # dense bf16 MFMA, MI355X_MICROARCH.md
 PEAK_FP32 = 157.3e12  # fp32 MFMA = vector rate
 PEAK_HBM = 8.0e12
+RECIPES = {"bf16x3": "bf16x3 recipe (split-bf16 hi+lo MFMA operands, fp32 accumulate; seed-3 parity)",
+           "bf16": "plain bf16 MFMA (fp32 accumulate)", "fp32": "fp32"}
 
 CONFIGS = {
     # name: (canvas, crop, patches per GPU, L, hidden layers)
@@ -105,42 +109,41 @@ def synthetic_inputs(B_total, h, w, device):
 
 
 def cpu_baseline(cfg, sample_patches):
-    """The CPU oracle (oracle/, numpy + C) on a bounded sample of the same workload: one training
-    step over `sample_patches` patches, 1 warm-up + timed steps for ~10-30 s.  Pixels/s."""
+    """SURVEY.md §8(d) CPU baseline: oracle/cpu_ref.py (op-for-op torch-CPU fp32 restatement of the
+    reference step, pinned to the reference's fixtures by tests/test_cpu_ref.py) on a bounded slice
+    of the same workload: `sample_patches` patches of the config, reference init (seed 3), c2f at
+    progress 0.2, torch threads = every core this process may run on, 2 warm-up + >= 5 timed
+    steps.  Pixels/s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        cores = os.cpu_count()
+    import cpu_ref
+    cores = cpu_ref.set_threads()
     canvas, crop, _, L, hidden = CONFIGS[cfg]
     if canvas is None:
         canvas_h, canvas_w, ch, cw = 360, 480, 180, 240
     else:
         canvas_h = canvas_w = canvas
         ch = cw = crop
-    rng = np.random.default_rng(0)
-    dims = [2 + 4 * L] + hidden + [3]
-    params = []
-    for a, b in zip(dims[:-1], dims[1:]):
-        bound = 1 / np.sqrt(a)
-        params.append((rng.uniform(-bound, bound, (b, a)).astype(np.float32),
-                       rng.uniform(-bound, bound, b).astype(np.float32)))
-    rgb = rng.random((sample_patches, 3, ch, cw)).astype(np.float32)
-    mask = (rng.random((sample_patches, 1, ch, cw)) < 0.85).astype(np.float32)
-    warp = (rng.standard_normal((sample_patches, 8)) * 0.01).astype(np.float32)
-    c = dict(H=canvas_h, W=canvas_w, patch_H=ch, patch_W=cw, L=L, c2f=[0, 0.4], max_iter=3000, lr=1e-3,
+    D = 2 + 4 * L
+    torch.manual_seed(3)
+    params, k_in = [], D
+    for li, k_out in enumerate(hidden + [3]):  # RNG-ordered reference init (model/planar.py:410-427)
+        lin = torch.nn.Linear(k_in, k_out)
+        if li == 0:
+            lin.weight.data *= np.sqrt(D / 2.)
+            lin.bias.data *= np.sqrt(D / 2.)
+        params.append((lin.weight.detach().numpy().copy(), lin.bias.detach().numpy().copy()))
+        k_in = k_out
+    rgb, mask, warp = synthetic_inputs(sample_patches, ch, cw, torch.device("cpu"))
+    c = dict(H=canvas_h, W=canvas_w, patch_H=ch, patch_W=cw, L=L, c2f=[0, 0.4], max_iter=10 ** 9, lr=1e-3,
              lr_warp=1e-3, fix_first=True, use_edges=False, alpha_initial=0.0, alpha_final=1.0)
-    st = oracle.PlanarStep(c, params, warp, rgb, mask)
-    st.progress = np.float32(0.2)
-    st.step()  # warm-up
+    st = cpu_ref.CpuRefStep(c, params, warp.numpy(), rgb.numpy(), mask.numpy())
     times = []
-    t_end = time.time() + 20.0
-    while len(times) < 2 or (time.time() < t_end and len(times) < 8):
-        t0 = time.time()
+    for i in range(7):
+        st.progress.data.fill_(0.2)
+        t0 = time.perf_counter()
         st.step()
-        times.append(time.time() - t0)
+        if i >= 2:
+            times.append(time.perf_counter() - t0)
     px = sample_patches * ch * cw
     cpu = "unknown CPU"
     try:
@@ -151,8 +154,34 @@ def cpu_baseline(cfg, sample_patches):
     except OSError:
         pass
     return {"value": px / float(np.mean(times)), "unit": "pixels/s", "cores": int(cores), "kind": "port", "cpu": cpu,
-            "sample": f"{sample_patches} patches x {ch}x{cw} px, {len(times)} timed oracle steps "
-                      f"(numpy fp32 sgemm + C prologue), mean {np.mean(times):.2f} s/step"}
+            "sample": f"{sample_patches} patches x {ch}x{cw} px of {cfg}, 2 warm-up + {len(times)} timed "
+                      f"oracle/cpu_ref.py steps (torch-CPU fp32, autograd, Adam), mean {np.mean(times):.2f} s/step"}
+
+
+def prologue_rate(graph, var, L, c2f, n=20):
+    """Achieved HBM rate of the step's input side (16 B/px target + mask reads),
+    from a prologue-only launch (marf_prologue_probe) timed with HIP events on torch's stream, the
+    stream the library launches on."""
+    import marf_hip
+    w = graph.warp_param.weight.detach()
+    eng = graph.neural_image.engine(w.device)
+    b0, b1 = graph.shard if graph.shard else (0, w.shape[0])
+    Hm = marf_hip.sl3_to_SL3(w[b0:b1].contiguous())
+    gt = var.images.rgb[b0:b1]
+    mask = var.images.masks[b0:b1]
+    prog = graph.neural_image.progress
+    args = (gt, mask, Hm, eng.H, eng.W, eng.patch_H, eng.patch_W, L, prog, c2f)
+    marf_hip.prologue_probe(*args)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        marf_hip.prologue_probe(*args)
+    e1.record()
+    e1.synchronize()
+    s = e0.elapsed_time(e1) / n / 1e3
+    nbytes = 16 * gt.shape[0] * gt.shape[2] * gt.shape[3]
+    return {"kernel": "prologue_probe", "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": s * 1e3,
+            "achieved": nbytes / s / 1e9, "unit": "GB/s", "peak": PEAK_HBM / 1e9, "frac": nbytes / s / PEAK_HBM}
 
 
 def main():
@@ -161,12 +190,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=list(CONFIGS))
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16x3", "fp32"])
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2f", action="store_true", help="barf_c2f None (BASELINE config 5: c2f on vs off)")
     ap.add_argument("--strong", type=int, default=0, metavar="PATCHES",
                     help="strong scaling: PATCHES in total split over the ranks (SURVEY §8d: 512)")
-    ap.add_argument("--cpu-sample-patches", type=int, default=2)
+    ap.add_argument("--cpu-sample-patches", type=int, default=4)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -268,20 +297,25 @@ def main():
             torch.distributed.all_reduce(tr, op=torch.distributed.ReduceOp.MAX)
         render_pps = world * px_local * n_render / float(tr)
 
-    # ---- roofline of the dominant kernel (HIP-event durations measured above, same stream)
+    # ---- roofline of the dominant kernel (HIP-event durations measured above, same stream).
+    #      the governing roof is bf16 MFMA; achieved = ALGORITHMIC FLOPs of one
+    #      launch (the fp32 reference's multiply-adds, 2 per MAC) / its average duration.  The split
+    #      recipe issues 3 MFMAs per forward MAC and 2 per dgrad MAC: that count is reported beside it
+    #      (mfma_*), not in `achieved`.  HBM: algorithmic 16 B/px (target + mask) + 12 B/px (rgb
+    #      out); the saved layer inputs / pre-activation gradients the weight-gradient kernels read
+    #      back are the design's own traffic (design_bytes_per_launch), not algorithmic.
     dims = [2 + 4 * L] + hidden + [3]
     Kp0 = (dims[0] + 31) // 32 * 32
     S = (b1 - b0) * ((h * w + 127) // 128 * 128)
-    layer_flops = [2 * a * b for a, b in zip(dims[:-1], dims[1:])]
-    kflops = {
+    sum_mac = sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+    fwd_mult, bwd_mult = (3, 2) if args.precision == "bf16x3" else (1, 1)
+    kflops = {  # (algorithmic, MFMA-issued) FLOPs per launch
         # fused step: forward + dgrad chain (incl. layer 0, for the warp gradient) + last-layer wgrad
-        "mlp_step": px_local * (2 * sum(layer_flops) + 2 * 3 * dims[-2]),
-        "mlp_fwd": S * sum(layer_flops),
-        "mlp_bwd_dgrad": S * sum(layer_flops),
-        "wgrad_hidden": S * 2 * hidden[0] * hidden[0],
-        "wgrad_l0": S * 2 * dims[0] * dims[1],
+        "mlp_step": (px_local * (4 * sum_mac + 6 * dims[-2]),
+                     px_local * ((2 * fwd_mult + 2 * bwd_mult) * sum_mac + 6 * dims[-2])),
+        "wgrad_hidden": (px_local * 2 * hidden[0] * hidden[0],) * 2,
+        "wgrad_l0": (px_local * 2 * dims[0] * dims[1],) * 2,
     }
-    kbytes = step_kernel_bytes(S, Kp0, hidden, 4 if args.precision == "fp32" else 2)
     per_kernel = {k: {"avg_ms": v[0] / v[1], "launches_per_step": v[1] / args.steps} for k, v in prof.items()}
     step_kernel_ms = sum(v[0] for v in prof.values()) / args.steps
     dom = max(prof.items(), key=lambda kv: kv[1][0])[0] if prof else None
@@ -289,32 +323,27 @@ def main():
     roof = None
     if dom in kflops:
         avg_s = prof[dom][0] / prof[dom][1] / 1e3
-        flops, nbytes = kflops[dom], kbytes.get(dom)
-        mfma = {"bound": "mfma", "achieved": flops / avg_s / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
-                "frac": flops / avg_s / peak, "algorithmic_flops_per_launch": flops}
-        hbm = None
-        if nbytes:
-            tr = pmc_traffic(args.config, args.precision, dom)
-            hbm = {"bound": "hbm", "achieved": nbytes / avg_s / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                   "frac": nbytes / avg_s / PEAK_HBM, "traffic": tr[0] if tr else None,
-                   "algorithmic_bytes_per_launch": nbytes}
-            if tr:
-                hbm["traffic_source"] = tr[1]
-        # the binding roof is the one with the larger lower bound on the kernel's time
-        if hbm and nbytes / PEAK_HBM >= flops / peak:
-            roof = dict(hbm, kernel=dom, avg_launch_ms=avg_s * 1e3, secondary=mfma)
-        else:
-            roof = dict(mfma, kernel=dom, avg_launch_ms=avg_s * 1e3, traffic=hbm["traffic"] if hbm else None,
-                        secondary=hbm)
+        alg, issued = kflops[dom]
+        alg_bytes = 28 * px_local if dom == "mlp_step" else None
+        design = step_kernel_bytes(S, Kp0, hidden, 2 if args.precision != "fp32" else 4).get(dom)
+        tr = pmc_traffic(args.config, args.precision, dom)
+        roof = {"bound": "mfma", "achieved": alg / avg_s / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
+                "frac": alg / avg_s / peak, "traffic": tr[0] if tr else None,
+                "kernel": dom, "avg_launch_ms": avg_s * 1e3, "algorithmic_flops_per_launch": alg,
+                "mfma_flops_per_launch": issued, "mfma_tflops": issued / avg_s / 1e12, "mfma_frac": issued / avg_s / peak,
+                "algorithmic_bytes_per_launch": alg_bytes, "design_bytes_per_launch": design,
+                "traffic_ratio": (tr[0] / alg_bytes) if (tr and alg_bytes) else None,
+                "traffic_source": tr[1] if tr else None}
+    prologue = prologue_rate(graph, var, L, opt.barf_c2f) if world == 1 or rank == 0 else None
     ms = elapsed / args.steps * 1e3
     value = world * px_local / (elapsed / args.steps)
     F = flops_per_px(dims)
     out = {
         "metric": METRIC, "value": value, "unit": "pixels/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
-        "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+        "vs_baseline": None, "dtype": args.precision, "data": "synthetic (procedural targets, Bernoulli masks, random warps; reference-style init)",
         "config": {"workload": f"{args.config}: {per_gpu} patches x {h}x{w} px per GPU, L={L}, MLP "
-                               f"{'-'.join(map(str, dims))}, {args.precision}, "
+                               f"{'-'.join(map(str, dims))}, {RECIPES[args.precision]}, "
                                + ("c2f off" if args.no_c2f else "c2f [0,0.4] at progress 0.2"),
                    "patches_per_gpu": per_gpu, "pixels_per_step_per_gpu": px_local,
                    "pixels_per_s_per_gpu": value / world, "parallelism": f"dp{world} (patches)",
@@ -324,6 +353,7 @@ def main():
                    "loss_rgb_last": loss_v,
                    "render_pixels_per_s": render_pps},
         "roofline": roof,
+        "prologue": prologue,
         "kernels": per_kernel,
         "kernel_ms_per_step": step_kernel_ms,
     }

@@ -76,6 +76,12 @@ int marf_warp_points(const float* d_xy, const float* d_H, float* d_uv, int B, in
 /* ---- Positional encoding + c2f (model/planar.py:451-471): [n][2] -> [n][4L] */
 int marf_posenc(const float* d_coord, long long n, int L, const marf_c2f* c2f, float* d_enc, void* stream);
 
+/* Measurement only (no reference counterpart): the fused step's per-pixel input side -- target +
+ * mask reads (16 B/px), pixel grid, warp, posenc + c2f -- as a standalone launch of `grid` blocks,
+ * one float per block into d_out, so the prologue's HBM rate can be timed. */
+int marf_prologue_probe(const marf_geometry* geo, const marf_c2f* c2f, int L, const float* d_gt, const float* d_mask,
+                        float* d_out, int grid, void* stream);
+
 /* ---- Neural image MLP (model/planar.py:395-449, NeuralImageFunction)
  * dims[0] = 2 + 4L (input), dims[n_layers] = 3, hidden dims arbitrary (padded internally).
  * Flat fp32 parameter vector layout = NeuralImageFunction.mlp parameters in module order:

@@ -242,6 +242,21 @@ int marf_posenc(const float* d_coord, long long n, int L, const marf_c2f* c2f, f
     return MARF_OK;
 }
 
+// Measurement only: the fused step's input side (target + mask reads, grid, warp, posenc) as its
+// own launch, so that the prologue's HBM rate can be timed.  d_out: `grid` floats.
+int marf_prologue_probe(const marf_geometry* geo, const marf_c2f* c2f, int L, const float* d_gt, const float* d_mask,
+                        float* d_out, int grid, void* stream) {
+    GeoDev g;
+    int rc = make_geo(geo, g, MARF_TILE_PAD);
+    if (rc != MARF_OK) return rc;
+    if (g.mode != MARF_GEO_GRID || L < 0 || L > 32 || !d_gt || !d_out || grid <= 0)
+        return fail(MARF_ERR_INVALID, "prologue_probe: bad arguments");
+    MarfProfScope ps("prologue_probe", (hipStream_t)stream);
+    HIPCHK(marf_launch_prologue_probe(g, make_c2f(c2f), L, d_gt, d_mask, d_out, grid, (hipStream_t)stream),
+           "prologue_probe");
+    return MARF_OK;
+}
+
 // ------------------------------------------------------------------ network
 
 int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** out) {

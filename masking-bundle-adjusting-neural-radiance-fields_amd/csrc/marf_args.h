@@ -160,3 +160,5 @@ hipError_t marf_launch_warp_points(const float* xy, const float* Hm, float* uv, 
                                    hipStream_t s);
 hipError_t marf_launch_posenc(const float* coord, long long n, int L, const float* progress, float start, float span,
                               int c2f_on, float* enc, hipStream_t s);
+hipError_t marf_launch_prologue_probe(const GeoDev& g, const marf::C2fDev& c, int L, const float* gt,
+                                      const float* mask, float* out, int grid, hipStream_t s);

@@ -218,6 +218,45 @@ __global__ void k_posenc(const float* __restrict__ coord, long long n, int L, co
     }
 }
 
+
+// Prologue probe (measurement only, SURVEY.md §8(d) "achieved prologue GB/s"): the fused step's
+// per-pixel input side on its own -- read the target r, g, b and the mask (16 B/px, fp32 planes),
+// pixel grid -> warp by the patch's H -> posenc + c2f features -- reduced to one float per block so
+// that nothing is optimised away.  bench.py divides 16 B/px by its HIP-event time.
+__global__ __launch_bounds__(256) void k_prologue_probe(GeoDev g, C2fDev c, int L, const float* __restrict__ gt,
+                                                        const float* __restrict__ mask, float* __restrict__ out) {
+    __shared__ float wl[32];
+    __shared__ float red[4];
+    if (threadIdx.x < 32) {
+        float w = 1.0f;
+        if (c.on && (int)threadIdx.x < L) w = c2f_weight(*c.progress, c.start, c.span, L, threadIdx.x);
+        wl[threadIdx.x] = w;
+    }
+    __syncthreads();
+    const long long n = (long long)g.B * g.Np;
+    float acc = 0.f;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const int b = (int)(i / g.Np), p = (int)(i - (long long)b * g.Np);
+        const float* t = gt + (size_t)b * 3 * g.Np + p;
+        const float m = mask ? mask[(size_t)b * g.Np + p] : 1.0f;
+        const float tsum = (t[0] + t[g.Np] + t[2 * (size_t)g.Np]) * m;
+        float x, y, u, v, X[3];
+        slot_point<true>(g, b, p, x, y, u, v, X);
+        float f = u + v;
+        for (int k = 0; k < L; ++k) {
+            float s0, c0, s1, c1;
+            band_sincos<true>(u, k, s0, c0);
+            band_sincos<true>(v, k, s1, c1);
+            f += wl[k] * ((s0 + c0) + (s1 + c1));
+        }
+        acc += f * tsum;
+    }
+    acc = wave_total63(acc);
+    if ((threadIdx.x & 63) == 63) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 }  // namespace marf
 
 using namespace marf;
@@ -279,5 +318,11 @@ hipError_t marf_launch_posenc(const float* coord, long long n, int L, const floa
                               int c2f_on, float* enc, hipStream_t s) {
     hipLaunchKernelGGL(k_posenc, dim3(grid_for(n * 2 * L)), dim3(256), 0, s, coord, n, L, progress, start, span,
                        c2f_on, enc);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_prologue_probe(const GeoDev& g, const C2fDev& c, int L, const float* gt, const float* mask,
+                                      float* out, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_prologue_probe, dim3(grid), dim3(256), 0, s, g, c, L, gt, mask, out);
     return hipGetLastError();
 }

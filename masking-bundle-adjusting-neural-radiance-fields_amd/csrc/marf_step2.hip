@@ -55,6 +55,9 @@ MARF_DEV void s2_glds4(const void* src, unsigned lds) {
 typedef uint32_t s2_u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t s2_u32x4 __attribute__((ext_vector_type(4)));
 MARF_DEV void s2_st8(void* dst, uint32_t a, uint32_t b) {
+#ifdef S2_DIAG_NOSTORE
+    return;
+#endif
     const s2_u32x2 v = {a, b};
     asm volatile("global_store_dwordx2 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
@@ -237,6 +240,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     unsigned dma_dst = 0;
     const char* dma_src = nullptr;
     auto dma_arm = [&]() {
+#ifdef S2_DIAG_NODMA
+        ++dma_stage;
+        if (++dma_prog == a.n_stages) dma_prog = 0;
+        return;
+#endif
         dma_dst = lds0 + (dma_stage % C::NSLOT) * C::SLOT + wave * C::PER_DMA * 1024;
         dma_src = a.prog + (size_t)dma_prog * C::SLOT + wave * C::PER_DMA * 1024 + lane * 16;
         dma_left = C::PER_DMA;
@@ -261,7 +269,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         if (c_stage + 1 < total) s2_wait_vm<C::D * ST + C::PER_DMA>();
         else s2_wait_vm<C::D * ST>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef S2_DIAG_NOBAR  // (S2_DIAG_* : timing-only diagnostic builds, results invalid)
         __builtin_amdgcn_s_barrier();
+#endif
         asm volatile("" ::: "memory");
         S2T_END(0);
         S2T_BEGIN(1);
@@ -312,16 +322,21 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
 
     // one 32-row output tile: acc (+)= A[ks] . B[ks] over NK k-steps from the slot
     //   MODE 0: plain; 1: split forward (hi.hi + hi.lo + lo.hi); 2: split dgrad (hi.B + lo.B)
-    auto nohook = [&](auto) {};
+    // With one wave per SIMD the issue is in order, so the filler work of a k-step goes INTO the
+    // gaps between its MFMAs (each gap hides ~24 cycles of issue): hook(ks, 0) after the first
+    // MFMA, hook(ks, 1) after the second (right after the first in plain mode), the A-ring refill
+    // of each register right after the last MFMA that reads it, the DMA piece after the last MFMA.
+    // sched_barrier pins that order (left alone the scheduler sinks each LDS read to right before
+    // its MFMA, exposing its latency, and bunches the VALU behind the MFMA chain).
+    auto nohook = [&](auto, auto) {};
     auto gemm = [&](f32x16& acc, const char* slot, const S2Frag* Bhi, const S2Frag* Blo, int nk, auto mode_tag,
                     auto nk_tag, auto&& hook) {
         constexpr int MODE = decltype(mode_tag)::value;
         constexpr int NK = decltype(nk_tag)::value;
+        typedef std::integral_constant<int, 0> P0;
+        typedef std::integral_constant<int, 1> P1;
         const bf16x8* ah = reinterpret_cast<const bf16x8*>(slot + lane * 16);
         const bf16x8* al = reinterpret_cast<const bf16x8*>(slot + C::LO + lane * 16);
-        // 4-deep register ring of A fragments; sched_barrier pins the issue order (left alone the
-        // scheduler sinks each LDS read to right before its MFMA and exposes its latency).  hook(ks)
-        // is VALU work of the previous row tile's epilogue, placed beside the MFMAs of step ks.
         constexpr int P = NK < 4 ? NK : 4;
         bf16x8 A0[4], A1[4];
 #pragma unroll
@@ -329,32 +344,72 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             A0[u] = ah[u * 64];
             if constexpr (MODE != 0) A1[u] = al[u * 64];
         }
+        // two accumulators, alternating MFMA by MFMA: a dependent MFMA right behind its producer
+        // waits for the producer's result once VALU fillers sit between them
+        f32x16 accB = (f32x16){};
         s2_sfor<NK>([&](auto ksc) {
             constexpr int ks = decltype(ksc)::value;
             constexpr int u = ks & 3;
+            constexpr bool refill = ks + P < NK;
             const bool live = NK != C::NK0 || ks < nk;
-            __builtin_amdgcn_sched_barrier(0);
-            if (live) {
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0[u], Bhi[ks].f, acc, 0, 0, 0);
-                if constexpr (MODE == 1) {
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0[u], Blo[ks].f, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[u], Bhi[ks].f, acc, 0, 0, 0);
-                } else if constexpr (MODE == 2) {
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[u], Bhi[ks].f, acc, 0, 0, 0);
-                }
-                hook(ksc);
+            auto piece = [&]() {
                 if constexpr (NK >= 2 * C::PER_DMA) {
                     if constexpr ((ks & 1) == 1) dma_piece();
                 } else {
                     dma_piece();
                 }
+            };
+            // MFMA j of the whole sequence goes to acc (j even) or accB (j odd)
+            auto mf = [&](auto jc, const bf16x8& x, const bf16x8& y) {
+                if constexpr ((decltype(jc)::value & 1) == 0) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc, 0, 0, 0);
+                else accB = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, accB, 0, 0, 0);
+            };
+            constexpr int PER = MODE == 0 ? 1 : (MODE == 1 ? 3 : 2);
+            typedef std::integral_constant<int, PER * ks> J0;
+            typedef std::integral_constant<int, PER * ks + 1> J1;
+            typedef std::integral_constant<int, PER * ks + 2> J2;
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (MODE == 0) {
+                if (live) {
+                    mf(J0(), A0[u], Bhi[ks].f);
+                    hook(ksc, P0());
+                    hook(ksc, P1());
+                }
+                if constexpr (refill) A0[u] = ah[(ks + P) * 64];
+                if (live) piece();
+            } else if constexpr (MODE == 2) {
+                if (live) {
+                    mf(J0(), A0[u], Bhi[ks].f);
+                    hook(ksc, P0());
+                }
+                if constexpr (refill) A0[u] = ah[(ks + P) * 64];
+                __builtin_amdgcn_sched_barrier(0);
+                if (live) {
+                    mf(J1(), A1[u], Bhi[ks].f);
+                    hook(ksc, P1());
+                }
+                if constexpr (refill) A1[u] = al[(ks + P) * 64];
+                if (live) piece();
+            } else {
+                if (live) {
+                    mf(J0(), A0[u], Bhi[ks].f);
+                    hook(ksc, P0());
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (live) {
+                    mf(J1(), A0[u], Blo[ks].f);
+                    hook(ksc, P1());
+                }
+                if constexpr (refill) A0[u] = ah[(ks + P) * 64];
+                __builtin_amdgcn_sched_barrier(0);
+                if (live) mf(J2(), A1[u], Bhi[ks].f);
+                if constexpr (refill) A1[u] = al[(ks + P) * 64];
+                if (live) piece();
             }
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (ks + P < NK) {
-                A0[u] = ah[(ks + P) * 64];
-                if constexpr (MODE != 0) A1[u] = al[(ks + P) * 64];
-            }
         });
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += accB[r];
     };
     typedef std::integral_constant<int, 0> M0t;
     typedef std::integral_constant<int, SPLIT ? 1 : 0> MFt;
@@ -420,13 +475,17 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     long long myslot_g = 0;
     struct EpSt {
         uint32_t bits, mw;
-        float vp;
+        float vp, xo;
         uint32_t hw[8], lw[8];
     } ep;
     f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
-    // forward step e: ReLU + mask bit of register e; the odd steps pack the (hi, lo) bf16 pair
-    auto fstep = [&](const f32x16& pa, auto ec) {
+    // forward step e: ReLU + mask bit of register e (frelu); the odd steps then pack the (hi, lo)
+    // bf16 pair of registers e-1, e (fpack)
+    auto frelu = [&](const f32x16& pa, auto ec) {
         constexpr int e = decltype(ec)::value;
+#ifdef S2_DIAG_NOEPI
+        return;
+#endif
         float x;
         asm volatile(
             "v_cmp_lt_f32_e32 vcc, 0, %2\n\t"
@@ -435,17 +494,48 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             : "=&v"(x), "+v"(ep.bits)
             : "v"(pa[e])
             : "vcc");
+        if constexpr (e & 1) ep.xo = x;
+        else ep.vp = x;
+    };
+    // (inline asm so that the IR passes cannot sink the packing to its use after the GEMM: it is
+    //  meant to run in the MFMA gap where the hook places it; v_cvt_pk_bf16_f32 rounds to nearest
+    //  even, as s2_pk)
+    auto fpack = [&](auto ec) {
+        constexpr int e = decltype(ec)::value;
+#ifdef S2_DIAG_NOEPI
+        return;
+#endif
         if constexpr (e & 1) {
-            const uint32_t w = s2_pk(ep.vp, x);
-            ep.hw[e >> 1] = w;
-            if constexpr (SPLIT) ep.lw[e >> 1] = s2_pk(ep.vp - s2_lo16(w), x - s2_hi16(w));
-        } else {
-            ep.vp = x;
+            if constexpr (SPLIT) {
+                uint32_t w, wl, t0, t1;
+                asm volatile(
+                    "v_cvt_pk_bf16_f32 %0, %4, %5\n\t"
+                    "v_lshlrev_b32_e32 %2, 16, %0\n\t"
+                    "v_and_b32_e32 %3, 0xffff0000, %0\n\t"
+                    "v_sub_f32_e32 %2, %4, %2\n\t"
+                    "v_sub_f32_e32 %3, %5, %3\n\t"
+                    "v_cvt_pk_bf16_f32 %1, %2, %3"
+                    : "=&v"(w), "=&v"(wl), "=&v"(t0), "=&v"(t1)
+                    : "v"(ep.vp), "v"(ep.xo));
+                ep.hw[e >> 1] = w;
+                ep.lw[e >> 1] = wl;
+            } else {
+                uint32_t w;
+                asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(ep.vp), "v"(ep.xo));
+                ep.hw[e >> 1] = w;
+            }
         }
+    };
+    auto fstep = [&](const f32x16& pa, auto ec) {
+        frelu(pa, ec);
+        fpack(ec);
     };
     // forward finish of tile rt: operand fragments of k-steps 2 rt, 2 rt + 1, mask word, 4 stores
     auto ffinish = [&](int l, auto rtc, bool save, u16* sbase, int sld) {
         constexpr int rt = decltype(rtc)::value;
+#ifdef S2_DIAG_NOEPI
+        return;
+#endif
         Oh[2 * rt].u = make_uint4(ep.hw[0], ep.hw[1], ep.hw[2], ep.hw[3]);
         Oh[2 * rt + 1].u = make_uint4(ep.hw[4], ep.hw[5], ep.hw[6], ep.hw[7]);
         if constexpr (SPLIT) {
@@ -460,14 +550,30 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     // dgrad step e: dz = acc * relu'(z) with the mask word ep.mw
     auto bstep = [&](const f32x16& pa, auto ec, auto rtc) {
         constexpr int e = decltype(ec)::value;
+#ifdef S2_DIAG_NOEPI
+        return;
+#endif
         constexpr int rt = decltype(rtc)::value;
-        const int m = __builtin_amdgcn_sbfe((int)ep.mw, 16 * (1 - (rt & 1)) + 15 - e, 1);
-        const float x = __int_as_float(__float_as_int(pa[e]) & m);
-        if constexpr (e & 1) ep.hw[e >> 1] = s2_pk(ep.vp, x);
-        else ep.vp = x;
+        constexpr int bit = 16 * (1 - (rt & 1)) + 15 - e;
+        float x;
+        asm volatile(  // x = relu'(z) ? acc : 0 from the mask bit (in the gap, as fpack)
+            "v_bfe_i32 %0, %1, %3, 1\n\t"
+            "v_and_b32_e32 %0, %0, %2"
+            : "=&v"(x)
+            : "v"(ep.mw), "v"(pa[e]), "n"(bit));
+        if constexpr (e & 1) {
+            uint32_t w;
+            asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(ep.vp), "v"(x));
+            ep.hw[e >> 1] = w;
+        } else {
+            ep.vp = x;
+        }
     };
     auto bfinish = [&](auto rtc, u16* sbase, int sld) {
         constexpr int rt = decltype(rtc)::value;
+#ifdef S2_DIAG_NOEPI
+        return;
+#endif
         Oh[2 * rt].u = make_uint4(ep.hw[0], ep.hw[1], ep.hw[2], ep.hw[3]);
         Oh[2 * rt + 1].u = make_uint4(ep.hw[4], ep.hw[5], ep.hw[6], ep.hw[7]);
         store_rt(sbase, sld, myslot_g, rt, Oh[2 * rt], Oh[2 * rt + 1]);
@@ -569,10 +675,13 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         dummies(STt());
                     } else {
                         ep.bits = 0;
-                        gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, [&](auto ksc) {
+                        gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, [&](auto ksc, auto pc) {
                             s2_sfor<MS>([&](auto jc) {
                                 constexpr int e = decltype(ksc)::value * MS + decltype(jc)::value;
-                                if constexpr (e < 16) fstep(prv, std::integral_constant<int, e>());
+                                if constexpr (e < 16) {
+                                    if constexpr (decltype(pc)::value == 0) frelu(prv, std::integral_constant<int, e>());
+                                    else fpack(std::integral_constant<int, e>());
+                                }
                             });
                         });
                         s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
@@ -704,8 +813,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         gemm(cur, slot, gB, gB, 1, MBt(), NK1t(), nohook);
                     } else {
                         ep.mw = mkl[(lmask * C::NMW + ((rt - 1) >> 1)) * 64 + lane];
-                        gemm(cur, slot + rt * 1024, gB, gB, 1, MBt(), NK1t(), [&](auto) {
-                            s2_sfor<16>([&](auto ec) { bstep(prv, ec, std::integral_constant<int, rt - 1>()); });
+                        gemm(cur, slot + rt * 1024, gB, gB, 1, MBt(), NK1t(), [&](auto, auto pc) {
+                            s2_sfor<8>([&](auto ec) {
+                                bstep(prv, std::integral_constant<int, 8 * decltype(pc)::value + decltype(ec)::value>(),
+                                      std::integral_constant<int, rt - 1>());
+                            });
                         });
                         bfinish(std::integral_constant<int, rt - 1>(), sbase, sld);
                     }
@@ -739,8 +851,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         dummies(STt());
                     } else {
                         ep.mw = mkl[(lmask * C::NMW + ((rt - 1) >> 1)) * 64 + lane];
-                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), [&](auto ksc) {
-                            bstep(prv, ksc, std::integral_constant<int, rt - 1>());
+                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), [&](auto ksc, auto pc) {
+                            if constexpr (decltype(pc)::value == 0) bstep(prv, ksc, std::integral_constant<int, rt - 1>());
                         });
                         bfinish(std::integral_constant<int, rt - 1>(), sbase, sld);
                     }
@@ -792,9 +904,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                     if constexpr (t == 0) {
                         gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), nohook);
                     } else {
-                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), [&](auto ksc) {
+                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), [&](auto ksc, auto pc) {
                             constexpr int ks = decltype(ksc)::value;
-                            if constexpr ((ks & 1) == 0) adj_band(prv, t - 1, std::integral_constant<int, ks / 2>());
+                            if constexpr ((ks & 1) == 0 && decltype(pc)::value == 0)
+                                adj_band(prv, t - 1, std::integral_constant<int, ks / 2>());
                         });
                         adj_raw(prv, t - 1);
                     }

@@ -37,6 +37,8 @@ _SIGS = {
     "marf_pixel_grid": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_vp, _c_vp]),
     "marf_warp_points": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp]),
     "marf_posenc": (_c_int, [_c_vp, _c_ll, _c_int, ctypes.POINTER(C2f), _c_vp, _c_vp]),
+    "marf_prologue_probe": (_c_int, [ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_int, _c_vp, _c_vp, _c_vp, _c_int,
+                                     _c_vp]),
     "marf_net_create": (_c_int, [_c_int, ctypes.POINTER(_c_int), _c_int, _c_int, ctypes.POINTER(_c_vp)]),
     "marf_net_destroy": (None, [_c_vp]),
     "marf_net_param_count": (_c_ll, [_c_vp]),
@@ -200,6 +202,19 @@ def make_c2f(progress, c2f):
         c.d_progress = progress.data_ptr()
         c.start, c.end, c.on = float(c2f[0]), float(c2f[1]), 1
     return c
+
+
+def prologue_probe(gt, mask, Hm, H, W, patch_H, patch_W, L, progress=None, c2f=None, grid=4096):
+    """Measurement only: the fused step's input side (16 B/px target + mask reads, grid, warp,
+    posenc) as one launch (marf_prologue_probe); returns the per-block partials."""
+    B = gt.shape[0]
+    geo = grid_geometry(B, H, W, patch_H, patch_W, _f32(Hm, "Hm"))
+    out = torch.empty(grid, device=gt.device, dtype=torch.float32)
+    cf = make_c2f(progress, c2f)
+    _check(lib().marf_prologue_probe(ctypes.byref(geo), ctypes.byref(cf), L, _ptr(_f32(gt, "gt")),
+                                     _ptr(None if mask is None else _f32(mask, "mask")), _ptr(out), grid,
+                                     _stream(gt)))
+    return out
 
 
 def posenc(coord, L, progress=None, c2f=None):
