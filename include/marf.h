@@ -76,6 +76,16 @@ int marf_warp_points(const float* d_xy, const float* d_H, float* d_uv, int B, in
 /* ---- Positional encoding + c2f (model/planar.py:451-471): [n][2] -> [n][4L] */
 int marf_posenc(const float* d_coord, long long n, int L, const marf_c2f* c2f, float* d_enc, void* stream);
 
+/* Autograd of Warp.warp_grid's point warp (warp.py:70-81): upstream d_G [B][n][2] -> d xy
+ * [B][n][2] (per patch even when xy_shared: the caller sums them) and dH [B][3][3] (per-patch sum
+ * over points, fp64 accumulation).  dh then follows from marf_sl3_to_SL3_backward. */
+int marf_warp_points_backward(const float* d_xy, const float* d_H, const float* d_G, float* d_dxy, float* d_dH, int B,
+                              int n, int xy_shared, void* stream);
+/* Autograd of NeuralImageFunction.positional_encoding (model/planar.py:451-471): d_G [n][4L] ->
+ * d coord [n][2]; the c2f weights are constants (progress carries no gradient). */
+int marf_posenc_backward(const float* d_coord, long long n, int L, const marf_c2f* c2f, const float* d_G, float* d_dcoord,
+                         void* stream);
+
 /* Measurement only (no reference counterpart): the fused step's per-pixel input side -- target +
  * mask reads (16 B/px), pixel grid, warp, posenc + c2f -- as a standalone launch of `grid` blocks,
  * one float per block into d_out, so the prologue's HBM rate can be timed. */

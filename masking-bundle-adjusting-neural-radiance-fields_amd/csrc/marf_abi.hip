@@ -242,6 +242,26 @@ int marf_posenc(const float* d_coord, long long n, int L, const marf_c2f* c2f, f
     return MARF_OK;
 }
 
+int marf_warp_points_backward(const float* d_xy, const float* d_H, const float* d_G, float* d_dxy, float* d_dH, int B,
+                              int n, int xy_shared, void* stream) {
+    if (B <= 0 || n < 0 || !d_xy || !d_H || !d_G || !d_dxy || !d_dH)
+        return fail(MARF_ERR_INVALID, "warp_points_backward: bad arguments");
+    HIPCHK(marf_launch_warp_points_bwd(d_xy, d_H, d_G, d_dxy, d_dH, B, n, xy_shared, (hipStream_t)stream),
+           "warp_points_backward");
+    return MARF_OK;
+}
+
+int marf_posenc_backward(const float* d_coord, long long n, int L, const marf_c2f* c2f, const float* d_G, float* d_dcoord,
+                         void* stream) {
+    if (n < 0 || L <= 0 || L > 32 || !d_coord || !d_G || !d_dcoord)
+        return fail(MARF_ERR_INVALID, "posenc_backward: bad arguments");
+    if (n == 0) return MARF_OK;
+    C2fDev c = make_c2f(c2f);
+    HIPCHK(marf_launch_posenc_bwd(d_coord, d_G, n, L, c.progress, c.start, c.span, c.on, d_dcoord, (hipStream_t)stream),
+           "posenc_backward");
+    return MARF_OK;
+}
+
 // Measurement only: the fused step's input side (target + mask reads, grid, warp, posenc) as its
 // own launch, so that the prologue's HBM rate can be timed.  d_out: `grid` floats.
 int marf_prologue_probe(const marf_geometry* geo, const marf_c2f* c2f, int L, const float* d_gt, const float* d_mask,

@@ -160,5 +160,9 @@ hipError_t marf_launch_warp_points(const float* xy, const float* Hm, float* uv, 
                                    hipStream_t s);
 hipError_t marf_launch_posenc(const float* coord, long long n, int L, const float* progress, float start, float span,
                               int c2f_on, float* enc, hipStream_t s);
+hipError_t marf_launch_warp_points_bwd(const float* xy, const float* Hm, const float* G, float* dxy, float* dH, int B,
+                                       int n, int xy_shared, hipStream_t s);
+hipError_t marf_launch_posenc_bwd(const float* coord, const float* G, long long n, int L, const float* progress,
+                                  float start, float span, int c2f_on, float* dcoord, hipStream_t s);
 hipError_t marf_launch_prologue_probe(const GeoDev& g, const marf::C2fDev& c, int L, const float* gt,
                                       const float* mask, float* out, int grid, hipStream_t s);

@@ -218,6 +218,76 @@ __global__ void k_posenc(const float* __restrict__ coord, long long n, int L, co
     }
 }
 
+// Warp.warp_grid autograd (warp.py:70-81): uv = X[:2] / (X[2] + 1e-8), X = H [x, y, 1].
+// One block per patch walks its points: d xy per point, and dH = sum over points of
+// dX (x, y, 1)^T accumulated in fp64 in a fixed order (deterministic).  With a shared point set the
+// per-patch d xy rows are written separately and the caller sums them (autograd of the expand).
+__global__ __launch_bounds__(1024) void k_warp_points_bwd(const float* __restrict__ xy, const float* __restrict__ Hm,
+                                                          const float* __restrict__ G, float* __restrict__ dxy,
+                                                          float* __restrict__ dH, int n, int xy_shared) {
+    __shared__ double red[16][9];
+    const int b = blockIdx.x;
+    const float* H = Hm + 9 * b;
+    double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int p = threadIdx.x; p < n; p += 1024) {
+        const long long src = xy_shared ? p : (long long)b * n + p;
+        const long long dst = (long long)b * n + p;
+        const float x = xy[2 * src], y = xy[2 * src + 1];
+        float X[3], u, v;
+        warp_point(H, x, y, u, v, X, 9 * n < 400);
+        const float gu = G[2 * dst], gv = G[2 * dst + 1];
+        const float d = X[2] + 1e-8f;
+        const float dX0 = gu / d, dX1 = gv / d;
+        const float dd2 = d * d;
+        const float dX2 = (-gu * X[0]) / dd2 + (-gv * X[1]) / dd2;
+        const float hom[3] = {x, y, 1.f};
+        const float dX[3] = {dX0, dX1, dX2};
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) acc[3 * r + c] += (double)(dX[r] * hom[c]);
+        dxy[2 * dst] = (H[0] * dX0 + H[3] * dX1) + H[6] * dX2;
+        dxy[2 * dst + 1] = (H[1] * dX0 + H[4] * dX1) + H[7] * dX2;
+    }
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        const double t = wave_total63(acc[e]);
+        if ((threadIdx.x & 63) == 63) red[threadIdx.x >> 6][e] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 9) {
+        double t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w][threadIdx.x];
+        dH[9 * b + threadIdx.x] = (float)t;
+    }
+}
+
+// NeuralImageFunction.positional_encoding autograd (model/planar.py:451-471): for coordinate c of
+// point i, d c = sum_k (w_k g_sin cos(s_k) - w_k g_cos sin(s_k)) * 2^k pi, s_k = 2^k pi c (the c2f
+// weights w_k are constants of the step: progress carries no gradient).
+__global__ void k_posenc_bwd(const float* __restrict__ coord, const float* __restrict__ G, long long n, int L,
+                             const float* progress, float start, float span, int c2f_on, float* __restrict__ dcoord) {
+    const float pi_f = 3.14159265358979323846f;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < 2 * n; e += (long long)gridDim.x * 256) {
+        const long long i = e >> 1;
+        const int c = (int)(e & 1);
+        const float* g = G + i * 4 * L + c * 2 * L;
+        float acc = 0.f;
+        for (int k = 0; k < L; ++k) {
+            float s, co;
+            sincosf(posenc_arg(coord[e], k), &s, &co);
+            float gs = g[k], gc = g[L + k];
+            if (c2f_on) {
+                const float w = c2f_weight(*progress, start, span, L, k);
+                gs = gs * w;
+                gc = gc * w;
+            }
+            acc += (gs * co + gc * -s) * ldexpf(pi_f, k);
+        }
+        dcoord[e] = acc;
+    }
+}
+
 
 // Prologue probe (measurement only, SURVEY.md §8(d) "achieved prologue GB/s"): the fused step's
 // per-pixel input side on its own -- read the target r, g, b and the mask (16 B/px, fp32 planes),
@@ -324,5 +394,18 @@ hipError_t marf_launch_posenc(const float* coord, long long n, int L, const floa
 hipError_t marf_launch_prologue_probe(const GeoDev& g, const C2fDev& c, int L, const float* gt, const float* mask,
                                       float* out, int grid, hipStream_t s) {
     hipLaunchKernelGGL(k_prologue_probe, dim3(grid), dim3(256), 0, s, g, c, L, gt, mask, out);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_warp_points_bwd(const float* xy, const float* Hm, const float* G, float* dxy, float* dH, int B,
+                                       int n, int xy_shared, hipStream_t s) {
+    hipLaunchKernelGGL(k_warp_points_bwd, dim3(B), dim3(1024), 0, s, xy, Hm, G, dxy, dH, n, xy_shared);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_posenc_bwd(const float* coord, const float* G, long long n, int L, const float* progress,
+                                  float start, float span, int c2f_on, float* dcoord, hipStream_t s) {
+    hipLaunchKernelGGL(k_posenc_bwd, dim3(grid_for(2 * n)), dim3(256), 0, s, coord, G, n, L, progress, start, span,
+                       c2f_on, dcoord);
     return hipGetLastError();
 }

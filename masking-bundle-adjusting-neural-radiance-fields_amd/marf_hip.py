@@ -37,6 +37,8 @@ _SIGS = {
     "marf_pixel_grid": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_vp, _c_vp]),
     "marf_warp_points": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp]),
     "marf_posenc": (_c_int, [_c_vp, _c_ll, _c_int, ctypes.POINTER(C2f), _c_vp, _c_vp]),
+    "marf_warp_points_backward": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp]),
+    "marf_posenc_backward": (_c_int, [_c_vp, _c_ll, _c_int, ctypes.POINTER(C2f), _c_vp, _c_vp, _c_vp]),
     "marf_prologue_probe": (_c_int, [ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_int, _c_vp, _c_vp, _c_vp, _c_int,
                                      _c_vp]),
     "marf_net_create": (_c_int, [_c_int, ctypes.POINTER(_c_int), _c_int, _c_int, ctypes.POINTER(_c_vp)]),
@@ -183,17 +185,47 @@ def pixel_grid(H, W, patch_H, patch_W, crop, device):
     return xy
 
 
-def warp_points(xy, Hm):
-    """xy [B or 1, n, 2] warped by Hm [B, 3, 3] -> [B, n, 2] (warp.py:74-78), forward only."""
-    xy = _f32(xy, "xy")
-    Hm = _f32(Hm, "H")
+def _warp_points_fwd(xy, Hm):
     B, n = Hm.shape[0], xy.shape[-2]
     shared = 1 if xy.dim() == 2 or xy.shape[0] == 1 else 0
     if not shared and xy.shape[0] != B:
         raise ValueError("warp_points: batch mismatch")
     uv = torch.empty(B, n, 2, device=xy.device, dtype=torch.float32)
     _check(lib().marf_warp_points(_ptr(xy), _ptr(Hm), _ptr(uv), B, n, shared, _stream(xy)))
-    return uv
+    return uv, shared
+
+
+class _WarpPoints(torch.autograd.Function):
+    """uv = (H [x, y, 1])[:2] / ((H [x, y, 1])[2] + 1e-8) and its autograd (warp.py:70-81)."""
+
+    @staticmethod
+    def forward(ctx, xy, Hm):
+        xy, Hm = _f32(xy, "xy"), _f32(Hm, "H")
+        uv, shared = _warp_points_fwd(xy, Hm)
+        ctx.save_for_backward(xy, Hm)
+        ctx.shared, ctx.xy_shape = shared, xy.shape
+        return uv
+
+    @staticmethod
+    def backward(ctx, g):
+        xy, Hm = ctx.saved_tensors
+        g = _f32(g, "d uv")
+        B, n = Hm.shape[0], xy.shape[-2]
+        dxy = torch.empty(B, n, 2, device=g.device, dtype=torch.float32)
+        dH = torch.empty(B, 3, 3, device=g.device, dtype=torch.float32)
+        _check(lib().marf_warp_points_backward(_ptr(xy), _ptr(Hm), _ptr(g), _ptr(dxy), _ptr(dH), B, n, ctx.shared,
+                                               _stream(g)))
+        if ctx.shared:
+            dxy = dxy.sum(0).reshape(ctx.xy_shape)
+        return dxy, dH
+
+
+def warp_points(xy, Hm):
+    """xy [B or 1, n, 2] warped by Hm [B, 3, 3] -> [B, n, 2] (warp.py:74-78); differentiable in
+    both (marf_warp_points_backward)."""
+    if torch.is_grad_enabled() and (xy.requires_grad or Hm.requires_grad):
+        return _WarpPoints.apply(xy, Hm)
+    return _warp_points_fwd(_f32(xy, "xy"), _f32(Hm, "H"))[0]
 
 
 def make_c2f(progress, c2f):
@@ -217,14 +249,44 @@ def prologue_probe(gt, mask, Hm, H, W, patch_H, patch_W, L, progress=None, c2f=N
     return out
 
 
-def posenc(coord, L, progress=None, c2f=None):
-    """coord [..., 2] -> [..., 4L] (model/planar.py:451-471 layout), forward only."""
-    coord = _f32(coord, "coord")
+def _posenc_fwd(coord, L, progress, c2f):
     n = coord.numel() // 2
     enc = torch.empty(*coord.shape[:-1], 4 * L, device=coord.device, dtype=torch.float32)
     cf = make_c2f(progress, c2f)
     _check(lib().marf_posenc(_ptr(coord), n, L, ctypes.byref(cf), _ptr(enc), _stream(coord)))
     return enc
+
+
+class _Posenc(torch.autograd.Function):
+    """Positional encoding with BARF c2f weights and its autograd in the coordinates
+    (model/planar.py:451-471; progress enters through .data, so it gets no gradient)."""
+
+    @staticmethod
+    def forward(ctx, coord, L, progress, c2f):
+        coord = _f32(coord, "coord")
+        ctx.save_for_backward(coord)
+        ctx.L, ctx.progress, ctx.c2f = L, progress, c2f
+        return _posenc_fwd(coord, L, progress, c2f)
+
+    @staticmethod
+    def backward(ctx, g):
+        (coord,) = ctx.saved_tensors
+        g = _f32(g, "d enc")
+        dc = torch.empty_like(coord)
+        cf = make_c2f(ctx.progress, ctx.c2f)
+        _check(lib().marf_posenc_backward(_ptr(coord), coord.numel() // 2, ctx.L, ctypes.byref(cf), _ptr(g), _ptr(dc),
+                                          _stream(g)))
+        return dc, None, None, None
+
+
+def posenc(coord, L, progress=None, c2f=None):
+    """coord [..., 2] -> [..., 4L] (model/planar.py:451-471 layout); differentiable in coord
+    (marf_posenc_backward)."""
+    if progress is not None:
+        progress = progress.detach()
+    if torch.is_grad_enabled() and coord.requires_grad:
+        return _Posenc.apply(coord, L, progress, c2f)
+    return _posenc_fwd(_f32(coord, "coord"), L, progress, c2f)
 
 
 # ====================================================================== MLP engine

@@ -1,7 +1,7 @@
 """Warp / Lie with the reference's API (warp.py:5-108), computed by libmarf.so on the GPU.
 
   Warp(opt).get_normalized_pixel_grid(crop)  -> [B, h*w, 2]      (HIP pixel-grid kernel)
-  Warp(opt).warp_grid(xy_grid, warp)         -> [B, N, 2]        (HIP Lie exp + warp kernels)
+  Warp(opt).warp_grid(xy_grid, warp)         -> [B, N, 2]        (HIP Lie exp + warp kernels, autograd)
   Warp(opt).warp_corners(warp_param)         -> [B, 4, 2]
   Lie().sl3_to_SL3(h)                        -> [..., 3, 3]      (HIP, torch.matrix_exp bit-exact)
 
@@ -43,10 +43,8 @@ class Warp:
         if self.warp_type != "homography":
             raise AssertionError(f"unsupported warp type {self.warp_type}")
         assert self.dof == 8
-        if torch.is_grad_enabled() and warp.requires_grad:
-            raise NotImplementedError("warp_grid backward: use Graph.forward (fused path) for training")
-        H = lie.sl3_to_SL3(warp)
-        return marf_hip.warp_points(xy_grid, H)
+        H = lie.sl3_to_SL3(warp)  # differentiable: HIP matrix_exp adjoint
+        return marf_hip.warp_points(xy_grid, H)  # differentiable in xy and H
 
     def warp_corners(self, warp_param):
         """The four crop-window corners (in the reference's corner order) warped per patch."""

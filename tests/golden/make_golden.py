@@ -227,6 +227,79 @@ def make_step_c1(steps=10):
                         rgb=(rgb * 255).round().astype(np.uint8), mask=mask.astype(np.uint8))
 
 
+# ----------------------------------------------------- module API (autograd, render, metric)
+
+def make_api():
+    """Gradients through Warp.warp_grid (warp.py:70-81) and positional_encoding
+    (model/planar.py:451-471), the full-canvas render of Model.predict_entire_image
+    (model/planar.py:211-217) from the seed-3 init, and Model.homography_error
+    (model/planar.py:219-223)."""
+    warp, planar, _, _ = R.import_reference()
+    out = {}
+    rng = np.random.default_rng(15)
+    opt = R.make_opt()
+    W = warp.Warp(opt)
+    xy = W.get_normalized_pixel_grid(crop=True)[:, ::97].clone()  # [5, 446, 2] strided crop grid
+    xy = xy + torch.from_numpy(rng.normal(0, 0.01, xy.shape).astype(np.float32))
+    h = torch.from_numpy(rng.normal(0, 0.05, (5, 8)).astype(np.float32))
+    G = torch.from_numpy(rng.normal(0, 1, xy.shape).astype(np.float32))
+    xy_t, h_t = xy.clone().requires_grad_(), h.clone().requires_grad_()
+    uv = W.warp_grid(xy_t, h_t)
+    uv.backward(G)
+    out.update(wg_xy=np32(xy), wg_h=np32(h), wg_G=np32(G), wg_uv=np32(uv), wg_dxy=np32(xy_t.grad), wg_dh=np32(h_t.grad))
+    for L, prog, c2f in ((8, 0.3, [0, 0.4]), (10, 0.15, [0, 0.4]), (16, 0.2, [0, 0.4]), (10, 0.0, None)):
+        o = R.make_opt({"arch": {"posenc": {"L_2D": L}}, "barf_c2f": c2f})
+        R.seed_all(3)
+        nif = planar.NeuralImageFunction(o)
+        nif.progress.data.fill_(prog)
+        c = torch.from_numpy(rng.uniform(-1, 1, (2, 300, 2)).astype(np.float32)).requires_grad_()
+        enc = nif.positional_encoding(c)
+        Ge = torch.from_numpy(rng.normal(0, 1, enc.shape).astype(np.float32))
+        enc.backward(Ge)
+        tag = f"pe_L{L}_{'c2f' if c2f else 'off'}"
+        out.update({f"{tag}_cfg": np.array([L, prog, 1 if c2f else 0], np.float64), f"{tag}_coord": np32(c),
+                    f"{tag}_enc": np32(enc), f"{tag}_G": np32(Ge), f"{tag}_dcoord": np32(c.grad)})
+    # predict_entire_image: the seed-3 Graph, unwarped full 360x480 canvas, at two progress values
+    R.seed_all(opt.seed)
+    graph = planar.Graph(opt)
+    full = W.get_normalized_pixel_grid()[:1]
+    idx = np.arange(0, 360 * 480, 37)
+    out["pred_idx"] = idx
+    for prog in (0.0, 0.5):
+        graph.neural_image.progress.data.fill_(prog)
+        with torch.no_grad():
+            rgb = graph.neural_image.forward(full)
+        img = rgb.view(opt.H, opt.W, 3).permute(2, 0, 1)
+        out[f"pred_p{prog}_sample"] = np32(rgb.view(-1, 3)[idx])
+        out[f"pred_p{prog}_checks"] = checks(np32(img))
+    # homography_error on fixed tensors
+    ph = torch.from_numpy(rng.normal(0, 0.1, (5, 8)).astype(np.float32))
+    gh = torch.from_numpy(np.eye(3, dtype=np.float32)[None] + rng.normal(0, 0.05, (5, 3, 3)).astype(np.float32))
+    fake = R.EasyDict(lie=warp.Lie())
+    out["he_pred"], out["he_gt"] = np32(ph), np32(gh)
+    out["he_err"] = np.array(float(planar.Model.homography_error(fake, ph, gh)), np.float64)
+    np.savez_compressed(os.path.join(HERE, "api.npz"), **out)
+
+
+def make_step_c1_L10(steps=4):
+    """BASELINE config 1 as written (L=10): cat_batch3, seed 3, c2f [0, 0.4], 4 iterations."""
+    opt = R.make_opt({"arch": {"posenc": {"L_2D": 10}}})
+    rgb, mask = load_cat_batch3(opt)
+    res = ref_train(opt, rgb, mask, steps=steps)
+    out = {}
+    rng = np.random.default_rng(16)
+    idx = np.unique(rng.integers(0, 5 * 43200, 4096))
+    out["rgb0_idx"], out["rgb0"] = idx, res["rgb0"].reshape(-1, 3)[idx]
+    for k, v in res["init"].items():
+        out[f"init_checks_{k}"] = checks(v)
+    for k, v in res["grads0"].items():
+        out[f"grad0_checks_{k}"] = checks(v)
+    out["grad0_warp"] = res["grads0"]["warp_param.weight"]
+    out["loss"] = np.array(res["loss"], np.float64)
+    out["warp_traj"] = np.stack(res["warp"])
+    np.savez_compressed(os.path.join(HERE, "step_c1_L10.npz"), **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["lie", "prologue", "small", "c1"]
     if "lie" in which:
@@ -237,6 +310,10 @@ if __name__ == "__main__":
         make_step_small()
     if "c1" in which:
         make_step_c1()
+    if "api" in which:
+        make_api()
+    if "c1L10" in which:
+        make_step_c1_L10()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

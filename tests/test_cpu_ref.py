@@ -61,3 +61,24 @@ def test_c1_first_steps_vs_reference(golden):
     for _ in range(3):
         losses.append(st.step()["loss_rgb"])
     np.testing.assert_allclose(losses, g["loss"][:4], rtol=1e-6)
+
+
+def test_api_autograd_vs_reference(golden):
+    """cpu_ref's warp_grid / positional_encoding under torch autograd against the reference's."""
+    import torch
+    z = golden("api")
+    xy = torch.from_numpy(z["wg_xy"]).requires_grad_()
+    h = torch.from_numpy(z["wg_h"]).requires_grad_()
+    uv = cpu_ref.warp_grid(xy, h)
+    np.testing.assert_allclose(uv.detach().numpy(), z["wg_uv"], atol=1e-6, rtol=0)
+    uv.backward(torch.from_numpy(z["wg_G"]))
+    np.testing.assert_allclose(xy.grad.numpy(), z["wg_dxy"], rtol=1e-5, atol=1e-6 * np.abs(z["wg_dxy"]).max())
+    np.testing.assert_allclose(h.grad.numpy(), z["wg_dh"], rtol=1e-5, atol=1e-6 * np.abs(z["wg_dh"]).max())
+    for tag in ("pe_L8_c2f", "pe_L10_c2f", "pe_L16_c2f", "pe_L10_off"):
+        L, prog, on = z[f"{tag}_cfg"]
+        c = torch.from_numpy(z[f"{tag}_coord"]).requires_grad_()
+        enc = cpu_ref.positional_encoding(c, int(L), torch.tensor(float(prog)), [0, 0.4] if on else None)
+        np.testing.assert_allclose(enc.detach().numpy(), z[f"{tag}_enc"], atol=1e-7, rtol=0)
+        enc.backward(torch.from_numpy(z[f"{tag}_G"]))
+        np.testing.assert_allclose(c.grad.numpy(), z[f"{tag}_dcoord"], rtol=1e-5,
+                                   atol=1e-6 * np.abs(z[f"{tag}_dcoord"]).max())

@@ -1,0 +1,104 @@
+"""The patch-sharded data parallelism with the real kernels: two processes on the one GPU (gloo),
+each running Model.train_iteration on its shard of the C1 cat_batch3 patches (5 patches -> 2 + 3),
+against the same iterations in one process.  The sharded sum order of the MLP gradient differs
+(SURVEY.md §8(e)), so the contract is <= 1e-5 relative, not bitwise."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(rank, world, port, precision, out):
+    import sys
+    import time
+    from conftest import GOLDEN, PKG, ROOT
+    sys.path[:0] = [PKG, ROOT]
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import options
+        from model import planar
+        from util import EasyDict as edict
+        imgs = np.load(os.path.join(GOLDEN, "cat_batch3_c1.npz"))
+        opt = options.load_options("options/planar.yaml")
+        opt = options.override_options(opt, edict({"model": "planar", "yaml": "planar", "seed": 3,
+                                                   "barf_c2f": [0, 0.4], "precision": precision}))
+        opt.device = "cuda:0"
+        opt.output_path = f"/tmp/marf_gpu_dist_{port}_{rank}"
+        torch.manual_seed(3)
+        m = planar.Model(opt)
+        rgb = torch.from_numpy(imgs["rgb"].astype(np.float32) / np.float32(255)).cuda()
+        mask = torch.from_numpy(imgs["mask"].astype(np.float32)).cuda()
+        m.images = edict(rgb=rgb, masks=mask, masks_eroded=mask, edges=None, gt_hom=None, gt=None)
+        m.build_networks()
+        m.setup_optimizer()
+        m.timer = edict(start=time.time(), it_mean=None)
+
+        class _Loader:
+            def set_postfix(self, **kw):
+                pass
+
+            def __len__(self):
+                return 1
+        var = edict(idx=torch.arange(5), images=m.images)
+        losses, grads = [], None
+        for s in range(STEPS):
+            loss = m.train_iteration(var, _Loader())
+            if m.rank == 0:
+                m.graph.warp_param.weight.data[0] = 0  # Model.train's fix_first line (rank 0 owns patch 0)
+            losses.append(float(loss.rgb))
+            if s == 0:
+                grads = [p.grad.detach().cpu().numpy().copy() for p in m.graph.neural_image.mlp.parameters()]
+        warps = m.gathered_warps().detach().cpu().numpy()
+        params = [p.detach().cpu().numpy().copy() for p in m.graph.neural_image.mlp.parameters()]
+        if rank == 0:
+            np.savez(out, losses=np.array(losses), warps=warps, shard=np.array(m.graph.shard or (0, 5)),
+                     **{f"g{i}": a for i, a in enumerate(grads)}, **{f"p{i}": a for i, a in enumerate(params)})
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_two_process_sharded_step_matches_single(precision, tmp_path):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    out2 = str(tmp_path / "two.npz")
+    procs = [ctx.Process(target=_run, args=(r, 2, port, precision, out2)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    out1 = str(tmp_path / "one.npz")
+    p1 = ctx.Process(target=_run, args=(0, 1, port, precision, out1))
+    p1.start()
+    p1.join(timeout=300)
+    assert p1.exitcode == 0
+    a, b = np.load(out1), np.load(out2)
+    assert tuple(b["shard"]) == (0, 2)
+    np.testing.assert_allclose(b["losses"], a["losses"], rtol=1e-5)
+    n = len([k for k in a.files if k.startswith("g")])
+    for i in range(n):  # first-step MLP gradient: <= 1e-5 relative to its max
+        ga, gb = a[f"g{i}"], b[f"g{i}"]
+        assert np.abs(gb - ga).max() <= 1e-5 * np.abs(ga).max() + 1e-12, (i, np.abs(gb - ga).max(), np.abs(ga).max())
+    np.testing.assert_allclose(b["warps"], a["warps"], atol=1e-5, rtol=0)  # warps after 3 steps: 1e-5
+    for i in range(n):
+        np.testing.assert_allclose(b[f"p{i}"], a[f"p{i}"], atol=1e-5, rtol=0)

@@ -671,34 +671,239 @@ def _run_c1(precision, tmp_path, iters=3000, fused=True, seed=3):
     return psnr, m.graph.warp_param.weight.detach().cpu().numpy()
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def _reference_runs():
+    """Final warps (patches 1-4) of the reference's own 3000-step seed-3 runs: SURVEY.md §6 (8 CPU
+    threads), and tests/golden/make_ref_runs.py here (4 threads; and the same with every MLP
+    parameter moved by one ulp).  The reference's final PSNR in those runs: 25.9968, 26.0499,
+    26.0868 dB; its warps differ between them by up to 3.2e-2, almost all of it an offset common to
+    every patch (5.5e-3 / 5.9e-3 once that offset is removed)."""
+    runs = [REF_WARPS_3000]
+    for tag in ("base", "ulp1"):
+        z = np.load(os.path.join(GOLDEN, f"ref_c1_3000_{tag}.npz"))
+        runs.append(z["warps"][-1][1:])
+    return runs
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
 def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path):
-    """BASELINE config 1/2 end to end: the seed=3 cat_batch3 run for 3000 iterations.
+    """BASELINE config 1/2 end to end: the seed=3 cat_batch3 run for 3000 iterations, for the recipe
+    the bench measures (bf16x3) and for fp32.
 
-    fp32: final PSNR within 0.05 dB of the reference's 25.9968 dB (north_star) and the recovered
-    warps within 3e-2 of the reference's.  The 6/10-step trajectories match to 1e-5
-    (test_c1_real_init_and_trajectory_fp32); over 3000 Adam steps the different fp32 summation
-    order (MFMA tiles vs the reference's CPU GEMMs) moves every patch by a common ~1-2e-2 offset
-    (measured: max 2.3e-2; our fused vs separate-kernel paths differ by as much).
-
-    bf16: the training outcome on this scene is set by which basin patch 1's perspective row falls
-    into (final PSNR ~22.7 / ~24.9 / ~26.0 dB), for fp32 as well: over 10 network-init seeds fp32
-    reaches 26.0 dB only on seed 3 (tools/seed_sweep.py; profiles/r1_seed_sweep.json, fp32 mean
-    23.92 dB vs bf16 23.66 dB).  Any rounding change (bf16 activations, or even fp16 posenc
-    features alone) re-rolls that basin, so the bf16 assertion is that the run trains into one of
-    the basins fp32 reaches (>= 22.5 dB) -- the 0.05 dB seed-3 bound is an fp32 property."""
+    PSNR: final within 0.05 dB of the reference's 25.9968 dB (north_star).
+    Warps: the north_star's 1e-2 cannot be met against a single reference run by the reference
+    itself -- its own reruns (other thread count, 1-ulp init) land up to 3.2e-2 apart, an offset
+    shared by all patches (_reference_runs).  What they do meet is 1e-2 on the patch-relative warps
+    (the common offset over patches 1-4 removed), and that is asserted here against the SURVEY run;
+    the absolute warps must lie within 3e-2 of the nearest reference run."""
     psnr, warps = _run_c1(precision, tmp_path)
+    runs = _reference_runs()
+    err = warps[1:] - REF_WARPS_3000
+    resid = err - err.mean(0, keepdims=True)
+    nearest = min(np.abs(warps[1:] - r).max() for r in runs)
     print(f"{precision}: final PSNR {psnr[-1]:.4f} dB, mean of last 10 logged {np.mean(psnr[-10:]):.4f} dB; "
-          f"max |warp - ref| {np.abs(warps[1:] - REF_WARPS_3000).max():.2e}")
-    print("warp - ref:\n", np.array2string(warps[1:] - REF_WARPS_3000, precision=4))
+          f"max |warp - ref| {np.abs(err).max():.2e} (patch-relative {np.abs(resid).max():.2e}, "
+          f"nearest reference run {nearest:.2e})")
+    print("warp - ref:\n", np.array2string(err, precision=4))
     print("PSNR every 300:", [round(x, 3) for x in psnr[14::15]])
     if os.environ.get("MARF_C1_SEPARATE"):
         p2, w2 = _run_c1(precision, tmp_path, fused=False)
         print(f"{precision} separate kernels: final PSNR {p2[-1]:.4f}; max |warp - fused| {np.abs(w2 - warps).max():.2e}")
-    if precision == "fp32":
-        assert abs(psnr[-1] - REF_PSNR_3000) <= 0.05, psnr[-10:]
-        np.testing.assert_allclose(warps[1:], REF_WARPS_3000, atol=3e-2)
-    else:
-        assert np.mean(psnr[-10:]) >= 22.5, psnr[-10:]
-        assert psnr[-1] > psnr[14] + 2.0, psnr[::15]  # trained well past the 300-step level
+    assert abs(psnr[-1] - REF_PSNR_3000) <= 0.05, psnr[-10:]
+    assert np.abs(resid).max() <= 1e-2, resid
+    assert nearest <= 3e-2, nearest
     assert np.all(warps[0] == 0)
+
+
+# ------------------------------------------------------------------------ C3 / C5 shapes vs the oracle
+
+def _synthetic_setup(precision, tmp_path, B, crop, L, hidden, c2f=(0, 0.4), progress=0.2, seed=3):
+    """A C3- or C5-shaped graph (512x512 canvas, crop x crop patches, L bands, hidden widths) with
+    seeded procedural targets, Bernoulli(0.85) masks and non-zero warps on every patch."""
+    from model import planar
+    from util import EasyDict as edict
+    opt = make_opt(tmp_path, H=512, W=512, patch_H=crop, patch_W=crop, batch_size=B, precision=precision,
+                   use_edges=False, arch={"layers": [None] + list(hidden) + [3], "skip": [], "posenc": {"L_2D": L}},
+                   barf_c2f=None if c2f is None else list(c2f))
+    torch.manual_seed(seed)
+    m = planar.Model(opt)
+    rng = np.random.default_rng(seed)
+    yy, xx = np.meshgrid(np.linspace(0, 1, crop), np.linspace(0, 1, crop), indexing="ij")
+    rgb = np.stack([[0.5 + 0.4 * np.sin(2 * np.pi * (rng.uniform(1, 4) * xx + rng.uniform(1, 4) * yy) + rng.uniform(0, 6))
+                     for _ in range(3)] for _ in range(B)]).astype(np.float32)
+    mask = (rng.random((B, 1, crop, crop)) < 0.85).astype(np.float32)
+    warp = (rng.standard_normal((B, 8)) * 0.01).astype(np.float32)
+    m.images = edict(rgb=t(rgb), masks=t(mask), masks_eroded=t(mask), edges=None, gt_hom=None, gt=None)
+    m.build_networks()
+    m.graph.warp_param.weight.data.copy_(t(warp))
+    m.graph.neural_image.progress.data.fill_(progress)
+    m.setup_optimizer()
+    params = [(m.graph.neural_image.mlp[i].weight.detach().cpu().numpy().copy(),
+               m.graph.neural_image.mlp[i].bias.detach().cpu().numpy().copy()) for i in range(len(hidden) + 1)]
+    cfg = dict(H=512, W=512, patch_H=crop, patch_W=crop, L=L, c2f=None if c2f is None else list(c2f), max_iter=3000,
+               lr=1e-3, lr_warp=1e-3, fix_first=True, use_edges=False, alpha_initial=0.0, alpha_final=1.0)
+    st = oracle.PlanarStep(cfg, params, warp, rgb, mask)
+    st.progress = np.float32(progress)
+    return m, edict(idx=torch.arange(B), images=m.images), st
+
+
+def _compare_step(m, var, st, precision, nl):
+    var, loss = one_step_grads(m, var)
+    r = st.step()
+    rgb = var.rgb_prediction.detach().cpu().numpy().reshape(-1, 3)
+    out = {"rgb": np.abs(rgb - r["rgb"]).max(), "loss": abs(float(loss.rgb) / float(r["loss_rgb"]) - 1)}
+    rel, cos = [], []
+    for i in range(nl):
+        for j, name in enumerate(("weight", "bias")):
+            got = getattr(m.graph.neural_image.mlp[i], name).grad.cpu().numpy()
+            ref = r["grads"][i][j]
+            rel.append(np.abs(got - ref).max() / (np.abs(ref).max() + 1e-30))
+            cos.append(float(got.ravel() @ ref.ravel() / (np.linalg.norm(got) * np.linalg.norm(ref) + 1e-30)))
+    dh = m.graph.warp_param.weight.grad.cpu().numpy()
+    out.update(grad_rel=max(rel), grad_cos=min(cos), dh_rel=np.abs(dh - r["dh"]).max() / np.abs(r["dh"]).max(),
+               dh_cos=float(dh.ravel() @ r["dh"].ravel() / (np.linalg.norm(dh) * np.linalg.norm(r["dh"]))))
+    print(precision, {k: float(v) for k, v in out.items()})
+    return out
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_c3_two_patch_step_vs_oracle(precision, tmp_path):
+    """C3 shape (256x256 crops of a 512 canvas, L=16, 4x256), 2 patches, non-zero warps on both:
+    rgb, loss, every MLP gradient and d warp against oracle.PlanarStep.
+    fp32: rgb <= 1e-5 abs, loss <= 1e-6 rel, gradients and dh <= 1e-5 relative to their max.
+    bf16x3 (the bench recipe, ~16 significant bits in the forward): rgb <= 1e-5 abs, gradients and
+    dh <= 1e-2 relative (north_star bf16 bound) with cosine >= 0.99999."""
+    m, var, st = _synthetic_setup(precision, tmp_path, 2, 256, 16, [256] * 4)
+    o = _compare_step(m, var, st, precision, 5)
+    assert o["rgb"] <= 1e-5
+    if precision == "fp32":
+        assert o["loss"] <= 1e-6 and o["grad_rel"] <= 1e-5 and o["dh_rel"] <= 1e-5, o
+    else:
+        assert o["loss"] <= 1e-5 and o["grad_rel"] <= 1e-2 and o["dh_rel"] <= 1e-2, o
+        assert o["grad_cos"] >= 0.99999 and o["dh_cos"] >= 0.99999, o
+
+
+@pytest.mark.parametrize("c2f", [(0, 0.4), None], ids=["c2f", "noc2f"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c5_shape_step_vs_oracle(precision, c2f, tmp_path):
+    """C5 shape (L=16, 8 hidden layers of 512; BASELINE config 5) at a reduced patch count (2 x
+    128x128), c2f on and off (barf_c2f None: no band weights and no layer-0 rescale).
+    fp32: rgb <= 1e-5 abs, gradients and dh <= 1e-5 relative.  bf16 (plain bf16 MFMA, the recipe
+    the library runs for widths above 256): rgb <= 1e-2 abs, gradient / dh cosine >= 0.99."""
+    m, var, st = _synthetic_setup(precision, tmp_path, 2, 128, 16, [512] * 8, c2f=c2f)
+    o = _compare_step(m, var, st, precision, 9)
+    if precision == "fp32":
+        assert o["rgb"] <= 1e-5 and o["grad_rel"] <= 1e-5 and o["dh_rel"] <= 1e-5, o
+    else:
+        assert o["rgb"] <= 1e-2 and o["grad_cos"] >= 0.99 and o["dh_cos"] >= 0.99, o
+
+
+# ------------------------------------------------------------------------ module API (autograd) and §8 rows a13 / f4
+
+def test_warp_grid_autograd_vs_reference(tmp_path):
+    """Warp.warp_grid differentiable in the points and the warp parameters (warp.py:70-81): d xy
+    and d h against the reference's autograd, <= 1e-5 relative to their max (fp32)."""
+    import warp as W
+    z = g("api")
+    wp = W.Warp(make_opt(tmp_path))
+    xy = t(z["wg_xy"]).requires_grad_()
+    h = t(z["wg_h"]).requires_grad_()
+    uv = wp.warp_grid(xy, h)
+    np.testing.assert_allclose(uv.detach().cpu().numpy(), z["wg_uv"], atol=1e-6, rtol=0)
+    uv.backward(t(z["wg_G"]))
+    for got, ref in ((xy.grad, z["wg_dxy"]), (h.grad, z["wg_dh"])):
+        got = got.cpu().numpy()
+        assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max(), np.abs(got - ref).max() / np.abs(ref).max()
+
+
+def test_warp_grid_autograd_shared_points(tmp_path):
+    """A [1, n, 2] point set broadcast over the patches: its gradient is the sum over patches."""
+    import warp as W
+    z = g("api")
+    wp = W.Warp(make_opt(tmp_path))
+    xy1 = t(z["wg_xy"][:1]).requires_grad_()
+    h = t(z["wg_h"])
+    wp.warp_grid(xy1, h).backward(t(z["wg_G"]))
+    xyB = t(np.repeat(z["wg_xy"][:1], 5, 0)).requires_grad_()
+    wp.warp_grid(xyB, h).backward(t(z["wg_G"]))
+    np.testing.assert_allclose(xy1.grad.cpu().numpy()[0], xyB.grad.sum(0).cpu().numpy(), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("tag", ["pe_L8_c2f", "pe_L10_c2f", "pe_L16_c2f", "pe_L10_off"])
+def test_positional_encoding_autograd_vs_reference(tag, tmp_path):
+    """NeuralImageFunction.positional_encoding differentiable in the coordinates
+    (model/planar.py:451-471): encoding <= 2.5e-7 abs, d coord <= 1e-5 relative to its max."""
+    from model import planar
+    z = g("api")
+    L, prog, on = z[f"{tag}_cfg"]
+    opt = make_opt(tmp_path, arch={"layers": [None, 256, 256, 256, 256, 3], "skip": [],
+                                   "posenc": {"L_2D": int(L)}}, barf_c2f=[0, 0.4] if on else None)
+    nif = planar.NeuralImageFunction(opt).to(DEV)
+    nif.progress.data.fill_(float(prog))
+    c = t(z[f"{tag}_coord"]).requires_grad_()
+    enc = nif.positional_encoding(c)
+    np.testing.assert_allclose(enc.detach().cpu().numpy(), z[f"{tag}_enc"], atol=2.5e-7, rtol=0)
+    enc.backward(t(z[f"{tag}_G"]))
+    ref = z[f"{tag}_dcoord"]
+    got = c.grad.cpu().numpy()
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max(), np.abs(got - ref).max() / np.abs(ref).max()
+    assert nif.progress.grad is None
+
+
+@pytest.mark.parametrize("prog", [0.0, 0.5])
+def test_predict_entire_image_vs_reference(prog, tmp_path):
+    """Model.predict_entire_image (model/planar.py:211-217): the seed-3 init rendered on the
+    unwarped 360x480 canvas, every 37th pixel against the reference, fp32 1e-5 abs."""
+    z = g("api")
+    m, _ = c1_setup("fp32", tmp_path)
+    m.graph.neural_image.progress.data.fill_(prog)
+    img = m.predict_entire_image()
+    assert tuple(img.shape) == (3, 360, 480)
+    got = img.permute(1, 2, 0).reshape(-1, 3).numpy()[z["pred_idx"]]
+    np.testing.assert_allclose(got, z[f"pred_p{prog}_sample"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(img.double().sum().item(), z[f"pred_p{prog}_checks"][0], rtol=1e-6)
+
+
+def test_homography_error_vs_reference(tmp_path):
+    """Model.homography_error (model/planar.py:219-223) on fixed tensors, fp32 1e-5 rel."""
+    z = g("api")
+    m, _ = c1_setup("fp32", tmp_path)
+    err = m.homography_error(t(z["he_pred"]), t(z["he_gt"]))
+    np.testing.assert_allclose(float(err), float(z["he_err"]), rtol=1e-5)
+
+
+def test_c1_L10_steps_vs_reference(tmp_path):
+    """BASELINE config 1 as written (L=10): cat_batch3, seed 3, 4 training iterations against the
+    reference.  rgb <= 1e-5 abs, loss <= 1e-5 rel, d warp <= 1e-4 relative to its max (a 5x8
+    reduction over 216,000 pixels in a different fp32 order), warps after 4 Adam steps <= 1e-5."""
+    z = g("step_c1_L10")
+    from model import planar
+    from util import EasyDict as edict
+    import time
+    imgs = g("cat_batch3_c1")
+    opt = make_opt(tmp_path, precision="fp32", arch={"layers": [None, 256, 256, 256, 256, 3], "skip": [],
+                                                     "posenc": {"L_2D": 10}})
+    torch.manual_seed(3)
+    m = planar.Model(opt)
+    rgb = t(imgs["rgb"].astype(np.float32) / np.float32(255))
+    mask = t(imgs["mask"].astype(np.float32))
+    m.images = edict(rgb=rgb, masks=mask, masks_eroded=mask, edges=None, gt_hom=None, gt=None)
+    m.build_networks()
+    m.setup_optimizer()
+    m.timer = edict(start=time.time(), it_mean=None)
+    var = edict(idx=torch.arange(5), images=m.images)
+    for i in range(5):
+        w = m.graph.neural_image.mlp[i].weight.detach().cpu().numpy().astype(np.float64)
+        np.testing.assert_allclose(w.sum(), z[f"init_checks_neural_image.mlp.{i}.weight"][0], rtol=1e-9)
+    losses = []
+    for s in range(4):
+        loss = m.train_iteration(var, _Loader())
+        if s == 0:
+            got = var.rgb_prediction.detach().cpu().numpy().reshape(-1, 3)[z["rgb0_idx"]]
+            np.testing.assert_allclose(got, z["rgb0"], atol=1e-5)
+            dh = m.graph.warp_param.weight.grad.cpu().numpy()
+            print("L10 dh rel err", np.abs(dh - z["grad0_warp"]).max() / np.abs(z["grad0_warp"]).max())
+            np.testing.assert_allclose(dh, z["grad0_warp"], atol=1e-4 * np.abs(z["grad0_warp"]).max())
+        m.graph.warp_param.weight.data[0] = 0
+        losses.append(float(loss.rgb))
+    np.testing.assert_allclose(losses, z["loss"], rtol=1e-5)
+    np.testing.assert_allclose(m.graph.warp_param.weight.detach().cpu().numpy(), z["warp_traj"][-1], atol=1e-5)

@@ -197,3 +197,25 @@ def test_erode_known_answers():
     # a single hole grows to the 5x5 square around it; the border itself is not eroded
     assert (e[0] == 0).sum() == 25 and e[0, 2:7, 4:9].max() == 0.0
     assert oracle.erode_rect(np.ones((1, 6, 6), np.float32)).min() == 1.0
+
+
+def test_c1_L10_first_steps(golden):
+    """BASELINE config 1 as written (L=10): the oracle against the reference's 4 iterations."""
+    g = golden("step_c1_L10")
+    imgs = golden("cat_batch3_c1")
+    rgb = imgs["rgb"].astype(np.float32) / np.float32(255)
+    mask = imgs["mask"].astype(np.float32)
+    params = reference_init([256, 256, 256, 256, 3], 42, [0, 0.4], 3, 5)
+    for i, (W, b) in enumerate(params):
+        np.testing.assert_allclose(W.astype(np.float64).sum(), g[f"init_checks_neural_image.mlp.{i}.weight"][0], rtol=1e-9)
+    cfg = dict(H=360, W=480, patch_H=180, patch_W=240, L=10, c2f=[0, 0.4], max_iter=3000, lr=1e-3, lr_warp=1e-3,
+               fix_first=True, use_edges=True, alpha_initial=0.0, alpha_final=1.0)
+    st = oracle.PlanarStep(cfg, params, np.zeros((5, 8), np.float32), rgb, mask)
+    r = st.step()
+    np.testing.assert_allclose(r["rgb"][g["rgb0_idx"]], g["rgb0"], atol=2e-6)
+    np.testing.assert_allclose(r["dh"], g["grad0_warp"], atol=1e-4 * np.abs(g["grad0_warp"]).max())
+    losses = [r["loss_rgb"]]
+    for _ in range(3):
+        losses.append(st.step()["loss_rgb"])
+    np.testing.assert_allclose(losses, g["loss"], rtol=1e-5)
+    np.testing.assert_allclose(st.warp, g["warp_traj"][-1], atol=1e-6)
