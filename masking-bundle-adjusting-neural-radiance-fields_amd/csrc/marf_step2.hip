@@ -62,6 +62,9 @@ MARF_DEV void s2_st8(void* dst, uint32_t a, uint32_t b) {
     asm volatile("global_store_dwordx2 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
 MARF_DEV void s2_st16(void* dst, uint4 u) {
+#ifdef S2_DIAG_NOSTORE
+    return;
+#endif
     const s2_u32x4 v = {u.x, u.y, u.z, u.w};
     asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
@@ -146,7 +149,7 @@ struct S2Cfg {
     static constexpr int LO = NKH * 1024;                  // byte offset of the lo fragments in a slot
     static constexpr int PER_DMA = SLOT / (NW * 1024);     // DMA instructions per wave per stage
     static constexpr int NSLOT = 3, D = 2;
-    static constexpr int ST = 4;                           // store instructions per wave per stage
+    static constexpr int ST = 2;                           // store instructions per wave per stage
     static constexpr int NK0 = 9;                          // max layer-0 k-steps (L <= 32)
     static constexpr int NTA = 5;                          // max adjoint row tiles (L <= 39)
     static constexpr int TPX = 32 * NW;                    // pixel slots per block tile
@@ -310,14 +313,19 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     typedef std::integral_constant<int, ST> STt;
     typedef std::integral_constant<int, ST - 1> ST1t;
     // (the stores of a row tile into a natural-order [S][ld] bf16 tensor: k-step ks of the lane's
-    //  pixel holds columns 16 ks + 4 h + 0..3 (elements 0-3) and 16 ks + 8 + 4 h + 0..3 (4-7))
+    //  pixel holds columns 16 ks + 4 h + 0..3 (dwords x, y) and 16 ks + 8 + 4 h + 0..3 (z, w); two
+    //  v_permlane32_swap exchange the lane halves' x, y <-> z, w so that lane (p, h) holds columns
+    //  16 ks + 8 h + 0..7 contiguously: one 16-B store per lane per k-step, 2 per row tile)
     auto store_rt = [&](u16* base, int ld, long long slot, int rt, const S2Frag& f0, const S2Frag& f1) {
         dma_flush();
-        u16* row = base + slot * ld;
-        s2_st8(row + 32 * rt + 4 * h, f0.u.x, f0.u.y);
-        s2_st8(row + 32 * rt + 8 + 4 * h, f0.u.z, f0.u.w);
-        s2_st8(row + 32 * rt + 16 + 4 * h, f1.u.x, f1.u.y);
-        s2_st8(row + 32 * rt + 24 + 4 * h, f1.u.z, f1.u.w);
+        u16* row = base + slot * ld + 32 * rt + 8 * h;
+        auto contig = [&](const S2Frag& f) -> uint4 {
+            const auto xz = __builtin_amdgcn_permlane32_swap(f.u.x, f.u.z, false, false);
+            const auto yw = __builtin_amdgcn_permlane32_swap(f.u.y, f.u.w, false, false);
+            return make_uint4(xz[0], yw[0], xz[1], yw[1]);
+        };
+        s2_st16(row, contig(f0));
+        s2_st16(row + 16, contig(f1));
     };
 
     // one 32-row output tile: acc (+)= A[ks] . B[ks] over NK k-steps from the slot
@@ -344,9 +352,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             A0[u] = ah[u * 64];
             if constexpr (MODE != 0) A1[u] = al[u * 64];
         }
-        // two accumulators, alternating MFMA by MFMA: a dependent MFMA right behind its producer
-        // waits for the producer's result once VALU fillers sit between them
-        f32x16 accB = (f32x16){};
         s2_sfor<NK>([&](auto ksc) {
             constexpr int ks = decltype(ksc)::value;
             constexpr int u = ks & 3;
@@ -359,10 +364,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                     dma_piece();
                 }
             };
-            // MFMA j of the whole sequence goes to acc (j even) or accB (j odd)
-            auto mf = [&](auto jc, const bf16x8& x, const bf16x8& y) {
-                if constexpr ((decltype(jc)::value & 1) == 0) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc, 0, 0, 0);
-                else accB = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, accB, 0, 0, 0);
+            // one accumulation chain (a second, alternating accumulator measured no faster, and
+            // any change of the summation order re-rolls the seed-3 basin: DESIGN.md §4)
+            auto mf = [&](auto, const bf16x8& x, const bf16x8& y) {
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc, 0, 0, 0);
             };
             constexpr int PER = MODE == 0 ? 1 : (MODE == 1 ? 3 : 2);
             typedef std::integral_constant<int, PER * ks> J0;
@@ -408,8 +413,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             }
             __builtin_amdgcn_sched_barrier(0);
         });
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] += accB[r];
     };
     typedef std::integral_constant<int, 0> M0t;
     typedef std::integral_constant<int, SPLIT ? 1 : 0> MFt;
@@ -486,14 +489,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
 #ifdef S2_DIAG_NOEPI
         return;
 #endif
+        // relu as a signed-integer max with 0 (negative floats and -0 are negative integers: exactly
+        // x > 0 ? x : 0), mask bit = (relu(x) != 0), shifted in: no VCC traffic
         float x;
+        uint32_t t;
         asm volatile(
-            "v_cmp_lt_f32_e32 vcc, 0, %2\n\t"
-            "v_cndmask_b32_e32 %0, 0, %2, vcc\n\t"
-            "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
-            : "=&v"(x), "+v"(ep.bits)
-            : "v"(pa[e])
-            : "vcc");
+            "v_max_i32_e32 %0, 0, %3\n\t"
+            "v_min_u32_e32 %2, 1, %0\n\t"
+            "v_lshl_or_b32 %1, %1, 1, %2"
+            : "=&v"(x), "+v"(ep.bits), "=&v"(t)
+            : "v"(pa[e]));
         if constexpr (e & 1) ep.xo = x;
         else ep.vp = x;
     };

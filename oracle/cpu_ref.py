@@ -32,15 +32,15 @@ def sl3_to_SL3(h):
     return torch.linalg.matrix_exp(A)
 
 
-def pixel_grid(H, W, ph, pw, crop=True):
+def pixel_grid(H, W, ph, pw, crop=True, dtype=torch.float32):
     """Pixel-centre coordinates in [-1, 1] scaled by the aspect norms, x fastest: [h*w, 2]."""
     norm_h, norm_w = H / max(H, W), W / max(H, W)
     if crop:
-        ys = torch.arange(H // 2 - ph // 2, H // 2 + ph // 2, dtype=torch.float32)
-        xs = torch.arange(W // 2 - pw // 2, W // 2 + pw // 2, dtype=torch.float32)
+        ys = torch.arange(H // 2 - ph // 2, H // 2 + ph // 2, dtype=dtype)
+        xs = torch.arange(W // 2 - pw // 2, W // 2 + pw // 2, dtype=dtype)
     else:
-        ys = torch.arange(H, dtype=torch.float32)
-        xs = torch.arange(W, dtype=torch.float32)
+        ys = torch.arange(H, dtype=dtype)
+        xs = torch.arange(W, dtype=dtype)
     y = ((ys + 0.5) / H * 2 - 1) * norm_h
     x = ((xs + 0.5) / W * 2 - 1) * norm_w
     Y, X = torch.meshgrid(y, x, indexing="ij")
@@ -56,13 +56,13 @@ def warp_grid(xy, h):
 
 def positional_encoding(coord, L, progress=None, c2f=None):
     """[..., 2] -> [..., 4L]: per coordinate sin bands then cos bands, BARF c2f weighting."""
-    freq = 2 ** torch.arange(L, dtype=torch.float32) * np.pi
+    freq = (2 ** torch.arange(L, dtype=coord.dtype) * np.pi).to(coord.device)
     spec = coord[..., None] * freq
     enc = torch.stack([spec.sin(), spec.cos()], -2).view(*coord.shape[:-1], -1)
     if c2f is not None:
         start, end = c2f
         a = (progress - start) / (end - start) * L
-        k = torch.arange(L, dtype=torch.float32)
+        k = torch.arange(L, dtype=coord.dtype, device=coord.device)
         wgt = (1 - (a - k).clamp_(min=0, max=1).mul_(np.pi).cos_()) / 2
         enc = (enc.view(-1, L) * wgt).view(enc.shape)
     return enc
@@ -74,9 +74,11 @@ class CpuRefStep:
     cfg keys as oracle.PlanarStep: H, W, patch_H, patch_W, L (0 = posenc off), c2f (None or
     [start, end]), max_iter, lr, lr_warp, fix_first, use_edges, alpha_initial, alpha_final.
     params: [(W [out, in], b [out]), ...]; warp [B, 8]; rgb [B, 3, h, w]; mask [B, 1, h, w].
+    dtype / device: torch.float32 on the CPU is the reference's arithmetic; float64 gives the
+    near-exact values the fp32 implementations are measured against (tests).
     """
 
-    def __init__(self, cfg, params, warp, rgb, mask):
+    def __init__(self, cfg, params, warp, rgb, mask, dtype=torch.float32, device="cpu"):
         self.cfg = cfg
         self.mlp = torch.nn.ModuleList()
         for W, b in params:
@@ -84,12 +86,16 @@ class CpuRefStep:
             lin.weight.data.copy_(torch.as_tensor(np.asarray(W, np.float32)))
             lin.bias.data.copy_(torch.as_tensor(np.asarray(b, np.float32)))
             self.mlp.append(lin)
-        self.progress = torch.nn.Parameter(torch.tensor(0.0))
-        self.warp = torch.nn.Parameter(torch.as_tensor(np.asarray(warp, np.float32)).clone())
-        self.rgb = torch.as_tensor(np.asarray(rgb, np.float32))
-        self.mask = torch.as_tensor(np.asarray(mask, np.float32))
+        self.mlp.to(device=device, dtype=dtype)
+
+        def T(a):
+            return torch.as_tensor(np.asarray(a, np.float32)).to(device=device, dtype=dtype)
+        self.progress = torch.nn.Parameter(torch.tensor(0.0, dtype=dtype, device=device))
+        self.warp = torch.nn.Parameter(T(warp).clone())
+        self.rgb = T(rgb)
+        self.mask = T(mask)
         self.B, _, self.h, self.w = self.rgb.shape
-        self.xy = pixel_grid(cfg["H"], cfg["W"], cfg["patch_H"], cfg["patch_W"], crop=True)
+        self.xy = pixel_grid(cfg["H"], cfg["W"], cfg["patch_H"], cfg["patch_W"], crop=True, dtype=dtype).to(device)
         self.it = 0
         self.optim = torch.optim.Adam([dict(params=list(self.mlp.parameters()) + [self.progress], lr=cfg["lr"]),
                                        dict(params=[self.warp], lr=cfg["lr_warp"])])
@@ -122,9 +128,10 @@ class CpuRefStep:
         self.progress.data.fill_(self.it / c["max_iter"])
         if c.get("fix_first", True):
             self.warp.data[0] = 0
-        return dict(loss_rgb=float(loss_rgb.detach()), rgb=rgb.detach().reshape(-1, 3).numpy(),
-                    grads=[(lin.weight.grad.numpy().copy(), lin.bias.grad.numpy().copy()) for lin in self.mlp],
-                    dh=self.warp.grad.numpy().copy())
+        return dict(loss_rgb=float(loss_rgb.detach()), rgb=rgb.detach().reshape(-1, 3).cpu().numpy(),
+                    grads=[(lin.weight.grad.cpu().numpy().copy(), lin.bias.grad.cpu().numpy().copy())
+                           for lin in self.mlp],
+                    dh=self.warp.grad.cpu().numpy().copy())
 
 
 def set_threads():

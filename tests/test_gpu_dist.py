@@ -62,7 +62,10 @@ def _run(rank, world, port, precision, out):
             loss = m.train_iteration(var, _Loader())
             if m.rank == 0:
                 m.graph.warp_param.weight.data[0] = 0  # Model.train's fix_first line (rank 0 owns patch 0)
-            losses.append(float(loss.rgb))
+            lv = loss.rgb.detach().reshape(1).double().cpu()
+            if world > 1:  # each rank's loss.rgb is its patches' share over the global denominator
+                dist.all_reduce(lv)
+            losses.append(float(lv))
             if s == 0:
                 grads = [p.grad.detach().cpu().numpy().copy() for p in m.graph.neural_image.mlp.parameters()]
         warps = m.gathered_warps().detach().cpu().numpy()

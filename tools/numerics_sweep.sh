@@ -8,7 +8,7 @@ for vp in "$@"; do
   v=${vp%%:*}; p=${vp##*:}
   if [ "$v" = default ]; then lib=$PWD/masking-bundle-adjusting-neural-radiance-fields_amd/lib/libmarf.so
   else lib=$PWD/masking-bundle-adjusting-neural-radiance-fields_amd/lib/libmarf_$v.so; fi
-  MARF_LIB=$lib timeout -k 10 900 python -u tools/seed_sweep.py --seeds $SEEDS --precisions $p \
+  MARF_LIB=$lib timeout -k 10 900 python -u tools/seed_sweep.py --seeds $SEEDS --precisions $p --perturb ${PERTURB:-0} \
     --out gpurun_out/ns_${v}_$p.json > gpurun_out/ns_${v}_$p.log 2>&1
   rc=$?
   tail -3 gpurun_out/ns_${v}_$p.log

@@ -26,19 +26,21 @@ def main():
     ap.add_argument("--seeds", type=int, nargs="+", default=list(range(8)))
     ap.add_argument("--precisions", nargs="+", default=["fp32", "bf16"])
     ap.add_argument("--iters", type=int, default=3000)
+    ap.add_argument("--perturb", type=int, nargs="+", default=[0],
+                    help="ulp-perturbation draws of the init (0 = none); each seed runs every draw")
     ap.add_argument("--out", default="gpurun_out/seed_sweep.json")
     a = ap.parse_args()
     res = []
     for prec in a.precisions:
-        for s in a.seeds:
+        for s, pt in [(s, pt) for s in a.seeds for pt in a.perturb]:
             t0 = time.time()
             with tempfile.TemporaryDirectory() as d:
-                psnr, w = T._run_c1(prec, d, iters=a.iters, seed=s)
-            r = dict(precision=prec, seed=s, psnr=float(psnr[-1]), psnr_mean10=float(np.mean(psnr[-10:])),
+                psnr, w = T._run_c1(prec, d, iters=a.iters, seed=s, perturb=pt)
+            r = dict(precision=prec, seed=s, perturb=pt, psnr=float(psnr[-1]), psnr_mean10=float(np.mean(psnr[-10:])),
                      warps=w.tolist(), secs=round(time.time() - t0, 1), lib=os.environ.get("MARF_LIB", "default"),
                      warp_err=float(np.abs(w[1:] - T.REF_WARPS_3000).max()), psnr_traj=[float(x) for x in psnr])
             res.append(r)
-            print(f"{prec:5s} seed {s}: final PSNR {r['psnr']:.3f} dB (mean of last 10 logged {r['psnr_mean10']:.3f}) "
+            print(f"{prec:5s} seed {s} perturb {pt}: final PSNR {r['psnr']:.3f} dB (mean of last 10 logged {r['psnr_mean10']:.3f}) "
                   f"max |warp - ref| {r['warp_err']:.3e} in {r['secs']} s [{r['lib']}]", flush=True)
             os.makedirs(os.path.dirname(a.out), exist_ok=True)
             json.dump(res, open(a.out, "w"))
