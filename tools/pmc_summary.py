@@ -69,8 +69,10 @@ if "--traffic" in sys.argv:
     for r in rows:
         k = r["kernel"]
         name = None
-        if k.startswith("k_mlp_step"):
+        if k.startswith("k_mlp_step") or k.startswith("k_step2"):
             name = "mlp_step"
+        elif k.startswith("k_prologue_probe"):
+            name = "prologue_probe"
         elif k.startswith("k_wgrad_dma<"):
             name = "wgrad_hidden" if k.rstrip(">").endswith("256") else "wgrad_l0"
         elif k.startswith("k_wgrad<"):
