@@ -800,7 +800,8 @@ def test_c3_two_patch_step_vs_oracle(precision, tmp_path):
     rgb <= 1e-5 abs and loss vs oracle.PlanarStep (fp32 <= 1e-6 rel).  Gradients against the
     float64 reference ops: fp32 within 1e-5 relative to their max OR within 2x the reference's own
     fp32 error, whichever is larger (_compare_step); bf16x3 (the bench recipe) within 1e-2 (north_star
-    bf16 bound) with cosine >= 0.99999."""
+    bf16 bound) AND within 2x the reference's own fp32 error (measured: MLP 4.9e-4 vs the
+    reference's 4.7e-4; d warp 6.9e-3 vs 5.3e-3 -- a 2 x 65,536-pixel sum that cancels)."""
     m, var, inputs = _synthetic_setup(precision, tmp_path, 2, 256, 16, [256] * 4)
     o = _compare_step(m, var, inputs, precision, 5)
     assert o["rgb"] <= 1e-5
@@ -810,7 +811,7 @@ def test_c3_two_patch_step_vs_oracle(precision, tmp_path):
         assert o["dh_err"] <= max(1e-5, 2 * o["dh_err_ref32"]), o
     else:
         assert o["loss"] <= 1e-5 and o["grad_err"] <= 1e-2 and o["dh_err"] <= 1e-2, o
-        assert o["grad_cos"] >= 0.99999 and o["dh_cos"] >= 0.99999, o
+        assert o["grad_err"] <= 2 * o["grad_err_ref32"] and o["dh_err"] <= 2 * o["dh_err_ref32"], o
 
 
 @pytest.mark.parametrize("c2f", [(0, 0.4), None], ids=["c2f", "noc2f"])
