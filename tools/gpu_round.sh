@@ -5,7 +5,7 @@ set -o pipefail
 TAG=${1:-r1}
 OUT=$PWD/gpurun_out
 mkdir -p $OUT
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf -p no:cacheprovider > $OUT/gpu_tests_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/gpu_tests_$TAG.log 2>&1
 RC=$?
 echo "pytest exit $RC" >> $OUT/gpu_tests_$TAG.log
 tail -3 $OUT/gpu_tests_$TAG.log
