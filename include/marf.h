@@ -120,6 +120,14 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
                   const void* d_saved, void* d_workspace, float* d_dparams, float* d_dh, float* d_dcoords,
                   void* stream);
 
+/* Forward-only render (Graph.forward / NeuralImageFunction.forward without autograd,
+ * model/planar.py:329-335, 429-449; Model.predict_entire_image :211-217) in the net's recipe: for
+ * split-bf16 nets the pixel-per-wave kernel on grid, canvas or explicit-coordinate geometry with a
+ * workspace of marf_render_workspace_bytes(); otherwise marf_forward (d_ws unused). */
+size_t marf_render_workspace_bytes(const marf_net* net, const marf_geometry* geo);
+int marf_render(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed, float* d_rgb,
+                void* d_ws, void* stream);
+
 /* ---- Fused training step (grid geometry).  Graph.forward + Graph.mse_loss (model/planar.py:329-336,
  * 382-391) and the backward of both, computed in one pass per pixel tile because the target and
  * mask are known at forward time.  marf_step_forward writes rgb [B][Np][3] (may be NULL), the loss

@@ -691,9 +691,11 @@ static bool use_step2(const marf_net* n) {
     return true;
 }
 
-static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p) {
+// render = a forward-only launch: no saved tensors, no dH / weight-gradient partials
+static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p, bool render = false) {
     const Step2NetPlan& q = n->s2;
     const int nl = n->n_layers;
+    const long long Ssave = render ? 0 : 1;
     p.S = (long long)g.B * g.Np_pad;
     p.n_tiles = (int)(p.S / (32 * q.NW));
     int cap = device_cus();
@@ -702,15 +704,15 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p)
     size_t off = 0;
     for (int l = 0; l < nl - 1; ++l) {
         p.feat[l] = off;
-        off += rup(p.S * (l == 0 ? q.ldf0 : n->Kp[l]) * 2, 256);
+        off += rup(Ssave * p.S * (l == 0 ? q.ldf0 : n->Kp[l]) * 2, 256);
     }
     p.dz[0] = 0;
     for (int l = 1; l < nl; ++l) {
         p.dz[l] = off;
-        off += rup(p.S * n->Kp[l] * 2, 256);
+        off += rup(Ssave * p.S * n->Kp[l] * 2, 256);
     }
     p.dH = off;
-    off += rup(p.S / 32 * 9 * 4, 256);
+    off += rup(Ssave * p.S / 32 * 9 * 4, 256);
     p.loss = off;
     off += rup((long long)p.grid * 2 * 8, 256);
     p.blast = off;
@@ -733,22 +735,22 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p)
         mxm = std::max(mxm, (long long)n->Mp[l]);
     }
     p.part = off;
-    off += rup(std::max(n_chunks * mxo, 256LL * (3 * q.Kl + 3)) * 4, 256);
+    off += rup(Ssave * std::max(n_chunks * mxo, 256LL * (3 * q.Kl + 3)) * 4, 256);
     p.bpart = off;
-    off += rup(n_chunks * mxm * 4, 256);
+    off += rup(Ssave * n_chunks * mxm * 4, 256);
     p.total = off;
 }
 
 static int step2_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
                          const float* d_gt, const float* d_mask, const float* d_denom_override, float* d_rgb,
-                         float* d_loss_out, void* d_saved, hipStream_t s) {
+                         float* d_loss_out, void* d_saved, hipStream_t s, bool render = false) {
     const Step2NetPlan& q = net->s2;
     Step2Args a;
     memset(&a, 0, sizeof(a));
     int rc = make_geo(geo, a.geo, 32 * q.NW);
     if (rc) return rc;
     Step2BufPlan p;
-    plan_step2_bufs(net, a.geo, p);
+    plan_step2_bufs(net, a.geo, p, render);
     char* sv = (char*)d_saved;
     const char* pk = (const char*)d_packed;
     const int nl = net->n_layers;
@@ -760,6 +762,12 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     a.c2f_on = cf.on;
     a.prog = pk + q.prog_off;
     a.n_stages = q.n_stages;
+    if (render) {  // the program's forward prefix: the layer-0 and hidden row tiles + the last layer
+        a.fwd_only = 1;
+        a.n_stages = 1;
+        for (int l = 0; l < nl - 1; ++l) a.n_stages += q.nrt[l];
+        a.pro_fallback = a.geo.mode == MARF_GEO_COORDS ? a.geo.coords : a.geo.Hm;
+    }
     a.bias = (const float*)(pk + q.bias_off);
     a.nbias = q.nbias;
     a.gt = d_gt;
@@ -772,8 +780,8 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
         y.boff = q.boff[l];
         y.ldf = l == 0 ? q.ldf0 : net->Kp[l];
         y.ldz = net->Kp[l];
-        y.feat = l < nl - 1 ? (u16*)(sv + p.feat[l]) : nullptr;
-        y.dz = l >= 1 ? (u16*)(sv + p.dz[l]) : nullptr;
+        y.feat = l < nl - 1 && !render ? (u16*)(sv + p.feat[l]) : nullptr;
+        y.dz = l >= 1 && !render ? (u16*)(sv + p.dz[l]) : nullptr;
     }
     a.dH_partial = (float*)(sv + p.dH);
     a.loss_partial = (double*)(sv + p.loss);
@@ -803,6 +811,11 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     if (net->L > 0) HIPCHK(marf_launch_c2f_weights(cf, net->L, (float*)(sv + p.c2f), s), "step_forward c2f");
     HIPCHK(hipMemcpyAsync(sv + p.kmap, pk + q.kmap_off, (size_t)net->D * 4, hipMemcpyDeviceToDevice, s),
            "step_forward kmap");
+    if (render) {
+        MarfProfScope ps("mlp_fwd", s);
+        HIPCHK(marf_launch_step2(a, q.variant, p.grid, s), "render step2");
+        return MARF_OK;
+    }
     {
         MarfProfScope ps("mlp_step", s);
         HIPCHK(marf_launch_step2(a, q.variant, p.grid, s), "step_forward step2");
@@ -863,6 +876,29 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                "step_backward warp");
     }
     return MARF_OK;
+}
+
+size_t marf_render_workspace_bytes(const marf_net* net, const marf_geometry* geo) {
+    if (!net || !geo || !use_step2(net)) return 0;
+    GeoDev g;
+    if (make_geo(geo, g, 32 * net->s2.NW) != MARF_OK) return 0;
+    Step2BufPlan p;
+    plan_step2_bufs(net, g, p, true);
+    return p.total;
+}
+
+int marf_render(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed, float* d_rgb,
+                void* d_ws, void* stream) {
+    if (!net || !geo || !d_packed || !d_rgb) return fail(MARF_ERR_INVALID, "render: NULL argument");
+    if (!use_step2(net)) return marf_forward(net, geo, c2f, d_packed, d_rgb, nullptr, stream);
+    if (!d_ws) return fail(MARF_ERR_INVALID, "render: workspace (marf_render_workspace_bytes) missing");
+    if (geo->mode == MARF_GEO_GRID || geo->mode == MARF_GEO_CANVAS) {
+        if (!geo->d_H) return fail(MARF_ERR_INVALID, "render: grid geometry needs d_H");
+    } else if (geo->mode == MARF_GEO_COORDS) {
+        if (geo->Np <= 0 || !geo->d_coords) return fail(MARF_ERR_INVALID, "render: coords geometry needs points");
+    }
+    return step2_forward(net, geo, c2f, d_packed, nullptr, nullptr, nullptr, d_rgb, nullptr, d_ws,
+                         (hipStream_t)stream, true);
 }
 
 size_t marf_step_saved_bytes(const marf_net* net, const marf_geometry* geo) {

@@ -102,6 +102,8 @@ struct Step2Args {
     float* dummy;                    // [grid][NW][ST][64][2] store sink
     unsigned long long* stamps;      // diagnostic builds (MARF_STAMPS): [grid][8] cycle totals of wave 0
     int n_tiles;                     // block tiles of 32 * NW pixel slots
+    int fwd_only;                    // render: forward stages only, rgb out, nothing saved
+    const float* pro_fallback;       // valid device address for the input DMA when gt / H are absent
     // LDS layout (byte offsets; computed on the host)
     int lds_pro, lds_bias, lds_c2f, lds_layers, lds_wave, lds_wave_bytes, lds_total;
 };

@@ -214,11 +214,13 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const int f = ((wave * 2 + i) * 64) + lane;   // float index in [0, 4 TPX)
             const int ch = f / C::TPX, q = f - ch * C::TPX;
             const int p = min(q0 + q, Np - 1);
-            const float* src = ch < 3 ? a.gt + ((size_t)b * 3 + ch) * Np + p
-                                      : (a.mask ? a.mask + (size_t)b * Np + p : a.gt + (size_t)b * 3 * Np + p);
+            const float* src = !a.gt ? a.pro_fallback
+                               : ch < 3 ? a.gt + ((size_t)b * 3 + ch) * Np + p
+                                        : (a.mask ? a.mask + (size_t)b * Np + p : a.gt + (size_t)b * 3 * Np + p);
             s2_glds4(src, __builtin_amdgcn_readfirstlane(base + (wave * 2 + i) * 256));
         }
-        s2_glds4(a.geo.Hm + 9 * (size_t)b + (lane < 9 ? lane : 0), __builtin_amdgcn_readfirstlane(base + 4 * C::TPX * 4));
+        s2_glds4(a.geo.Hm ? a.geo.Hm + 9 * (size_t)b + (lane < 9 ? lane : 0) : a.pro_fallback,
+                 __builtin_amdgcn_readfirstlane(base + 4 * C::TPX * 4));
     };
 
     // ---- the weight ring
@@ -440,40 +442,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     auto zero_out = [&](S2Frag& o0, S2Frag& o1, S2Frag& q0, S2Frag& q1) {
         o0.u = o1.u = q0.u = q1.u = make_uint4(0, 0, 0, 0);
     };
-    auto relu_out = [&](f32x16& acc, int l, int rt, S2Frag& o0, S2Frag& o1, S2Frag& q0, S2Frag& q1) {
-        uint32_t bits = 0;
-        float v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            float x;
-            asm volatile(
-                "v_cmp_lt_f32_e32 vcc, 0, %2\n\t"
-                "v_cndmask_b32_e32 %0, 0, %2, vcc\n\t"
-                "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
-                : "=&v"(x), "+v"(bits)
-                : "v"(acc[r])
-                : "vcc");
-            v[r] = x;
-        }
-        if ((rt & 1) == 0) mpend = bits << 16;
-        else mkl[(l * C::NMW + (rt >> 1)) * 64 + lane] = mpend | bits;
-        s2_split8<SPLIT>(v, o0, q0);
-        s2_split8<SPLIT>(v + 8, o1, q1);
-    };
-    // dgrad epilogue: dz = acc * relu'(z) with the forward's mask word
-    auto mask_out = [&](f32x16& acc, int lmask, int rt, S2Frag& o0, S2Frag& o1) {
-        const uint32_t w = mkl[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
-        float v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int m = __builtin_amdgcn_sbfe((int)w, 16 * (1 - (rt & 1)) + 15 - r, 1);
-            v[r] = __int_as_float(__float_as_int(acc[r]) & m);
-        }
-        S2Frag dumm;
-        s2_split8<false>(v, o0, dumm);
-        s2_split8<false>(v + 8, o1, dumm);
-    };
-
     // pipelined epilogues: micro-steps of one 32-row accumulator tile
     long long myslot_g = 0;
     struct EpSt {
@@ -604,7 +572,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
 #pragma unroll
         for (int e = 0; e < 9; ++e) Hm[e] = pro[4 * C::TPX + e];
         float x, y, u, v, X[3];
-        {
+        if (a.geo.mode == 1) {  // explicit coordinates (GeoDev mode 1; render only)
+            const int pc = min(p, Np - 1);
+            u = x = a.geo.coords[2 * (size_t)pc];
+            v = y = a.geo.coords[2 * (size_t)pc + 1];
+            X[0] = u;
+            X[1] = v;
+            X[2] = 1.0f;
+        } else {
             const int r = p / a.geo.w, cc = p - r * a.geo.w;
             x = grid_coord(a.geo.x0 + cc, a.geo.W, a.geo.norm_w);
             y = grid_coord(a.geo.y0 + r, a.geo.H, a.geo.norm_h);
@@ -646,11 +621,13 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                     F0l[g] = rl;
                 }
             // feat_0 (bf16 hi) for the layer-0 weight gradient: column 16 ks + 8 h + j
-            u16* row = ly_ptr(0, 0) + myslot * ly_int(0, 3);
+            if (!a.fwd_only) {
+                u16* row = ly_ptr(0, 0) + myslot * ly_int(0, 3);
 #pragma unroll
-            for (int g = 0; g < C::NK0; ++g)
-                if (g < a.nk0) s2_st16(row + 16 * g + 8 * h, F0h[g].u);
-            if (16 * a.nk0 < ly_int(0, 3)) s2_st16(row + 16 * a.nk0 + 8 * h, make_uint4(0, 0, 0, 0));
+                for (int g = 0; g < C::NK0; ++g)
+                    if (g < a.nk0) s2_st16(row + 16 * g + 8 * h, F0h[g].u);
+                if (16 * a.nk0 < ly_int(0, 3)) s2_st16(row + 16 * a.nk0 + 8 * h, make_uint4(0, 0, 0, 0));
+            }
         }
 
         S2T_END(4);
@@ -661,7 +638,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         auto fwd_layer = [&](int l, const S2Frag* Bhi, const S2Frag* Blo, int nk, auto nk_tag, auto ms_tag) {
             constexpr int MS = decltype(ms_tag)::value;  // epilogue micro-steps beside each k-step
             const int nrt = ly_int(l, 0);
-            const bool save = l + 1 < nl - 1;
+            const bool save = l + 1 < nl - 1 && !a.fwd_only;
             u16* sbase = save ? ly_ptr(l + 1, 0) : nullptr;
             const int sld = save ? ly_int(l + 1, 3) : 0;
             const int boff = ly_int(l, 2);
@@ -748,6 +725,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             dma_flush();
             s2_st12(o, yv[0], yv[1], yv[2]);
             dummies(ST1t());
+        }
+        if (a.fwd_only) {  // render: the program holds the forward stages only
+            S2T_END(6);
+            continue;
         }
         // g operand of the last-layer dgrad: lane half 0, k = [g hi (3), 0, g lo (3), 0]
         S2Frag Bg;

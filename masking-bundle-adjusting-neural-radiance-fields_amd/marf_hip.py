@@ -52,6 +52,8 @@ _SIGS = {
     "marf_backward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_vp, _c_vp, _c_int, _c_vp,
                                _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_step_saved_bytes": (_c_sz, [_c_vp, ctypes.POINTER(Geometry)]),
+    "marf_render_workspace_bytes": (_c_sz, [_c_vp, ctypes.POINTER(Geometry)]),
+    "marf_render": (_c_int, [_c_vp, ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_step_forward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_vp, _c_vp, _c_vp, _c_vp,
                                    _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_step_backward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
@@ -400,8 +402,11 @@ class _MLPFunction(torch.autograd.Function):
         if need_grad:
             saved = torch.empty(max(engine.net.saved_bytes(geo), 1), dtype=torch.uint8, device=coords.device)
         cf = make_c2f(progress, engine.c2f)
-        _check(lib().marf_forward(engine.net.handle, ctypes.byref(geo), ctypes.byref(cf), _ptr(packed), _ptr(rgb),
-                                  _ptr(saved), _stream(coords)))
+        if need_grad:
+            _check(lib().marf_forward(engine.net.handle, ctypes.byref(geo), ctypes.byref(cf), _ptr(packed), _ptr(rgb),
+                                      _ptr(saved), _stream(coords)))
+        else:
+            _render(engine, geo, cf, packed, rgb, _stream(coords))
         if need_grad:
             ctx.save_for_backward(c2, progress, rgb)
             ctx.coord_shape = coords.shape
@@ -651,9 +656,17 @@ def render_nograd(warp_weight, progress, engine, params, b0, b1):
     rgb = torch.empty(Bl, geo_np(engine), 3, device=w.device, dtype=torch.float32)
     packed = engine.packed_for(params)
     cf = make_c2f(progress, engine.c2f)
-    _check(lib().marf_forward(engine.net.handle, ctypes.byref(geo), ctypes.byref(cf), _ptr(packed), _ptr(rgb), None,
-                              st))
+    _render(engine, geo, cf, packed, rgb, st)
     return rgb
+
+
+def _render(engine, geo, cf, packed, rgb, st):
+    """marf_render: forward only in the net's recipe (the split-bf16 pixel-per-wave kernel for
+    bf16x3 nets, whose workspace is a small per-device buffer)."""
+    nb = lib().marf_render_workspace_bytes(engine.net.handle, ctypes.byref(geo))
+    ws = _BUFS.get("render_ws", nb, rgb.device) if nb else None
+    _check(lib().marf_render(engine.net.handle, ctypes.byref(geo), ctypes.byref(cf), _ptr(packed), _ptr(rgb), _ptr(ws),
+                             st))
 
 
 def mlp_forward(coords, progress, engine, params):

@@ -886,12 +886,14 @@ def test_positional_encoding_autograd_vs_reference(tag, tmp_path):
     assert nif.progress.grad is None
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("prog", [0.0, 0.5])
-def test_predict_entire_image_vs_reference(prog, tmp_path):
+def test_predict_entire_image_vs_reference(prog, precision, tmp_path):
     """Model.predict_entire_image (model/planar.py:211-217): the seed-3 init rendered on the
-    unwarped 360x480 canvas, every 37th pixel against the reference, fp32 1e-5 abs."""
+    unwarped 360x480 canvas, every 37th pixel against the reference, 1e-5 abs (fp32, and the
+    split-bf16 render: the pixel-per-wave kernel on explicit coordinates, forward stages only)."""
     z = g("api")
-    m, _ = c1_setup("fp32", tmp_path)
+    m, _ = c1_setup(precision, tmp_path)
     m.graph.neural_image.progress.data.fill_(prog)
     img = m.predict_entire_image()
     assert tuple(img.shape) == (3, 360, 480)
@@ -944,3 +946,25 @@ def test_c1_L10_steps_vs_reference(tmp_path):
         losses.append(float(loss.rgb))
     np.testing.assert_allclose(losses, z["loss"], rtol=1e-5)
     np.testing.assert_allclose(m.graph.warp_param.weight.detach().cpu().numpy(), z["warp_traj"][-1], atol=1e-5)
+
+
+def test_render_bf16x3_vs_oracle(tmp_path):
+    """Forward-only rendering in the bf16x3 recipe (marf_render -> the pixel-per-wave kernel with
+    the forward stages only): Graph.forward without grad on the C3 grid of 2 warped patches, and
+    NeuralImageFunction.forward on ragged explicit coordinates, against the oracle, 1e-5 abs."""
+    m, var, inputs = _synthetic_setup("bf16x3", tmp_path, 2, 256, 16, [256] * 4)
+    cfg, params, warp, rgb, mask, progress = inputs
+    st = oracle.PlanarStep(cfg, params, warp, rgb, mask)
+    st.progress = np.float32(progress)
+    ref = st.forward()["rgb"]
+    with torch.no_grad():
+        got = m.graph.forward(var, mode="eval").rgb_prediction.cpu().numpy().reshape(-1, 3)
+    assert np.abs(got - ref).max() <= 1e-5, np.abs(got - ref).max()
+    rng = np.random.default_rng(5)
+    for n in (1, 129, 1000 + 37):
+        c = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        with torch.no_grad():
+            out = m.graph.neural_image.forward(t(c)).cpu().numpy()
+        w = oracle.c2f_weights(np.float32(progress), [0, 0.4], 16)
+        _, r = oracle.mlp_forward(oracle.posenc_features(c, 16, w), params)
+        assert np.abs(out - r).max() <= 1e-5, (n, np.abs(out - r).max())
