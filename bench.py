@@ -196,6 +196,8 @@ def main():
     ap.add_argument("--strong", type=int, default=0, metavar="PATCHES",
                     help="strong scaling: PATCHES in total split over the ranks (SURVEY §8d: 512)")
     ap.add_argument("--cpu-sample-patches", type=int, default=4)
+    ap.add_argument("--no-render", action="store_true",
+                    help="skip the forward-only render rate (PMC passes: its launches share the step kernel's name)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -283,19 +285,21 @@ def main():
 
     # ---- forward-only render rate (reported beside the step): Graph.forward without
     #      grad = grid -> warp -> posenc -> MLP -> rgb over the same patches (k_mlp_fwd, no saves)
+    render_pps = None
     with torch.no_grad():
-        for _ in range(2):
+        for _ in range(0 if args.no_render else 2):
             graph.forward(var, mode="eval")
-        barrier()
-        t0 = time.perf_counter()
-        n_render = max(5, args.steps // 2)
-        for _ in range(n_render):
-            graph.forward(var, mode="eval")
-        barrier()
-        tr = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-        if world > 1:
-            torch.distributed.all_reduce(tr, op=torch.distributed.ReduceOp.MAX)
-        render_pps = world * px_local * n_render / float(tr)
+        if not args.no_render:
+            barrier()
+            t0 = time.perf_counter()
+            n_render = max(5, args.steps // 2)
+            for _ in range(n_render):
+                graph.forward(var, mode="eval")
+            barrier()
+            tr = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+            if world > 1:
+                torch.distributed.all_reduce(tr, op=torch.distributed.ReduceOp.MAX)
+            render_pps = world * px_local * n_render / float(tr)
 
     # ---- roofline of the dominant kernel (HIP-event durations measured above, same stream).
     #      the governing roof is bf16 MFMA; achieved = ALGORITHMIC FLOPs of one
