@@ -1,7 +1,9 @@
 """train.py end to end on the GPU box (SURVEY.md §8(a) a12 + the CLI of the reference's train.py:11-31):
-the pre-decoded cat_batch3 inputs (--dataset_npz), seed 3, c2f [0, 0.4], a few hundred iterations
-in the benchmarked bf16x3 recipe and in fp32.  Checks that the run completes, writes its options
-and scalar log, and that the logged PSNR follows the reference's early trajectory."""
+the pre-decoded cat_batch3 inputs (--dataset_npz), seed 3, c2f [0, 0.4], the full 3000 iterations
+(progress = it / max_iter drives the c2f schedule, so a shorter run is a different experiment) in
+the benchmarked bf16x3 recipe and in fp32, frames every 100 iterations.  Checks that the run
+completes, writes its options, scalar log and frames, and that the final logged PSNR is within
+0.05 dB of the reference's 25.9968 dB."""
 import json
 import os
 import subprocess
@@ -21,18 +23,15 @@ def test_train_py_dataset_npz(precision, tmp_path):
         pytest.skip("no GPU")
     cmd = [sys.executable, "train.py", "--group=smoke", "--model=planar", "--yaml=planar", f"--name={precision}",
            "--seed=3", "--barf_c2f=[0,0.4]", f"--dataset_npz={os.path.join(GOLDEN, 'cat_batch3_c1.npz')}",
-           f"--precision={precision}", "--max_iter=300", f"--output_root={tmp_path}"]
-    r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=240)
+           f"--precision={precision}", f"--output_root={tmp_path}"]
+    r = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True, timeout=270)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    out = tmp_path / "smoke" / precision
+    out = tmp_path / "smoke" / f"{precision}_seed3"  # the run name gains _seed<N> (options.py:99-104)
     assert (out / "options.yaml").exists()
     rows = [json.loads(x) for x in (out / "metrics.jsonl").read_text().splitlines()]
     psnr = {row["step"]: row["train/PSNR"] for row in rows}
-    assert sorted(psnr)[:3] == [20, 40, 60] and max(psnr) == 300, sorted(psnr)
-    # the reference's own run passes 19.5 dB at iteration 300 (tests/golden/ref_c1_3000_base.npz)
-    import numpy as np
-    ref = np.load(os.path.join(GOLDEN, "ref_c1_3000_base.npz"))
-    ref300 = float(ref["psnr"][list(ref["its"]).index(300)])
-    print(precision, {k: round(v, 3) for k, v in sorted(psnr.items())}, "reference at 300:", ref300)
-    assert psnr[300] > psnr[20] + 2.0
-    assert abs(psnr[300] - ref300) < 0.5, (psnr[300], ref300)
+    assert sorted(psnr)[:3] == [20, 40, 60] and max(psnr) == 3000, sorted(psnr)[-3:]
+    frames = sorted(int(f.split(".")[0]) for f in os.listdir(out / "vis"))  # frame 0 + one per 100 iterations
+    assert frames == list(range(31)), frames
+    print(precision, {k: round(v, 3) for k, v in sorted(psnr.items()) if k % 300 == 0})
+    assert abs(psnr[3000] - 25.9968) <= 0.05, psnr[3000]
