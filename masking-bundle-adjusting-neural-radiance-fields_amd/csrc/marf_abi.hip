@@ -46,6 +46,7 @@ static inline long long rup(long long x, long long m) { return (x + m - 1) / m *
 struct Step2NetPlan {
     int variant;           // -1: not available for this net; 0: bf16 (8 waves); 1: split bf16 (4 waves)
     int NW, HM, MAXR, NMW, slot, nk0, nta, n_stages, nbias, Kl, ldf0;
+    int r0, ns0;           // layer-0 row tiles per stage (their k-steps share one slot) and its stages
     int nrt[MARF_MAX_LAYERS], nrtb[MARF_MAX_LAYERS], boff[MARF_MAX_LAYERS];
     size_t prog_off, bias_off, kmap_off, end_off;
 };
@@ -101,7 +102,10 @@ static void plan_step2_net(marf_net* n) {
         bo += l == nl - 1 ? 32 : n->Mp[l];
     }
     q.nbias = bo;
-    for (int l = 0; l < nl - 1; ++l) st += q.nrt[l];
+    q.r0 = std::max(1, std::min(q.nrt[0], (q.HM / 16) / q.nk0));
+    q.ns0 = (q.nrt[0] + q.r0 - 1) / q.r0;
+    st += q.ns0;
+    for (int l = 1; l < nl - 1; ++l) st += q.nrt[l];
     st += 2;  // last layer forward, last-layer dgrad (every row tile in one stage)
     for (int l = nl - 2; l >= 1; --l) st += q.nrtb[l];
     st += q.nta;
@@ -397,6 +401,8 @@ int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, vo
         b.split = q.variant == 1;
         b.slot_bytes = q.slot;
         b.n_stages = q.n_stages;
+        b.r0 = q.r0;
+        b.ns0 = q.ns0;
         for (int l = 0; l <= net->n_layers; ++l) b.dims[l] = net->dims[l];
         for (int l = 0; l < net->n_layers; ++l) {
             b.nrt[l] = q.nrt[l];
@@ -758,14 +764,15 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     a.L = net->L;
     a.nk0 = q.nk0;
     a.nta = q.nta;
+    a.r0 = q.r0;
     C2fDev cf = make_c2f(c2f);
     a.c2f_on = cf.on;
     a.prog = pk + q.prog_off;
     a.n_stages = q.n_stages;
     if (render) {  // the program's forward prefix: the layer-0 and hidden row tiles + the last layer
         a.fwd_only = 1;
-        a.n_stages = 1;
-        for (int l = 0; l < nl - 1; ++l) a.n_stages += q.nrt[l];
+        a.n_stages = 1 + q.ns0;
+        for (int l = 1; l < nl - 1; ++l) a.n_stages += q.nrt[l];
         a.pro_fallback = a.geo.mode == MARF_GEO_COORDS ? a.geo.coords : a.geo.Hm;
     }
     a.bias = (const float*)(pk + q.bias_off);

@@ -85,6 +85,7 @@ struct S2Layer {
 struct Step2Args {
     GeoDev geo;                      // Np_pad is a multiple of 32 * NW
     int nl, L, nk0, nta, c2f_on;
+    int r0;                          // layer-0 row tiles per stage
     const char* prog;                // weight stage program: n_stages slots of SLOT bytes
     int n_stages;
     const float* bias;               // padded biases
@@ -110,6 +111,7 @@ struct Step2Args {
 
 struct Pack2Args {
     int nl, L, nk0, nta, NKH, split, slot_bytes, n_stages;
+    int r0, ns0;                     // layer-0 row tiles per stage, layer-0 stages
     int dims[MARF_MAX_LAYERS + 1];   // true widths
     int nrt[MARF_MAX_LAYERS], nrtb[MARF_MAX_LAYERS];
     long long w_off[MARF_MAX_LAYERS], b_off[MARF_MAX_LAYERS];  // flat parameter offsets

@@ -642,12 +642,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             u16* sbase = save ? ly_ptr(l + 1, 0) : nullptr;
             const int sld = save ? ly_int(l + 1, 3) : 0;
             const int boff = ly_int(l, 2);
+            const char* slot0 = nullptr;
             s2_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;
                 f32x16& cur = (rt & 1) ? acc1 : acc0;
                 f32x16& prv = (rt & 1) ? acc0 : acc1;
                 if (rt < nrt) {
-                    const char* slot = stage_begin();
+                    // layer 0: r0 row tiles share a stage (their few k-steps fill one slot)
+                    const int sub = l == 0 ? rt % a.r0 : 0;
+                    if (sub == 0) slot0 = stage_begin();
+                    const char* slot = slot0 + sub * a.nk0 * 1024;
                     // the next tile's target / mask / H into the other input buffer (the tile that
                     // read it last finished before this stage's barrier)
                     if (l == 0 && rt == 0 && it + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
@@ -1052,9 +1056,9 @@ __global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog
         int layer = -1, kind = -1, rt = 0;  // kind 0 fwd, 1 last fwd, 2 last dgrad, 3 hidden dgrad, 4 adjoint
         {
             int s = st;
-            if (s < a.nrt[0]) { layer = 0; kind = 0; rt = s; }
+            if (s < a.ns0) { layer = 0; kind = 0; rt = s; }  // rt = the layer-0 stage here
             else {
-                s -= a.nrt[0];
+                s -= a.ns0;
                 for (int l = 1; l < a.nl - 1 && kind < 0; ++l) {
                     if (s < a.nrt[l]) { layer = l; kind = 0; rt = s; }
                     else s -= a.nrt[l];
@@ -1081,9 +1085,11 @@ __global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog
             const float* W = params + a.w_off[layer];
             int m = -1, k = -1;  // W[m][k]
             if (kind == 0 && layer == 0) {
-                if (ks < a.nk0) {
-                    m = 32 * rt + r32;
-                    k = s2_l0_fwd_feature(ks, hh, j, a.L, a.nk0);
+                // a layer-0 stage holds r0 row tiles: tile rt r0 + r at fragment slots r nk0 ..
+                const int r = ks / a.nk0, kk = ks - r * a.nk0, rtt = rt * a.r0 + r;
+                if (r < a.r0 && rtt < a.nrt[0]) {
+                    m = 32 * rtt + r32;
+                    k = s2_l0_fwd_feature(kk, hh, j, a.L, a.nk0);
                 }
             } else if (kind == 0 || kind == 1) {
                 m = 32 * rt + r32;
