@@ -190,7 +190,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=list(CONFIGS))
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16", "fp32"])
+    ap.add_argument("--precision", default=None, choices=["bf16x3", "bf16", "fp32"],
+                    help="default bf16x3 (the seed-3 parity recipe); c5's 512-wide layers: bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2f", action="store_true", help="barf_c2f None (BASELINE config 5: c2f on vs off)")
     ap.add_argument("--strong", type=int, default=0, metavar="PATCHES",
@@ -199,6 +200,8 @@ def main():
     ap.add_argument("--no-render", action="store_true",
                     help="skip the forward-only render rate (PMC passes: its launches share the step kernel's name)")
     args = ap.parse_args()
+    if args.precision is None:  # split-bf16 keeps 256-wide activations in registers: c5 runs plain bf16
+        args.precision = "bf16" if max(CONFIGS[args.config][4]) > 256 else "bf16x3"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

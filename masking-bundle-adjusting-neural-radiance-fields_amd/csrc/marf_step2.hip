@@ -392,7 +392,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 if constexpr (refill) A0[u] = ah[(ks + P) * 64];
                 __builtin_amdgcn_sched_barrier(0);
                 if (live) {
+#ifndef S2_BWD_NO_W_LO  // numerics experiment: dgrad with W_hi^T only
                     mf(J1(), A1[u], Bhi[ks].f);
+#endif
                     hook(ksc, P1());
                 }
                 if constexpr (refill) A1[u] = al[(ks + P) * 64];
@@ -404,12 +406,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (live) {
+#ifndef S2_FWD_NO_ACT_LO  // numerics experiment: activations carried as bf16 hi only
                     mf(J1(), A0[u], Blo[ks].f);
+#endif
                     hook(ksc, P1());
                 }
                 if constexpr (refill) A0[u] = ah[(ks + P) * 64];
                 __builtin_amdgcn_sched_barrier(0);
+#ifndef S2_FWD_NO_W_LO  // numerics experiment: forward weights bf16 hi only
                 if (live) mf(J2(), A1[u], Bhi[ks].f);
+#endif
                 if constexpr (refill) A1[u] = al[(ks + P) * 64];
                 if (live) piece();
             }
