@@ -45,7 +45,7 @@ static inline long long rup(long long x, long long m) { return (x + m - 1) / m *
 // step2 plan (the pixel-per-wave fused step, marf_step2.hip), filled by plan_step2_net
 struct Step2NetPlan {
     int variant;           // -1: not available for this net; 0: bf16 (8 waves); 1: split bf16 (4 waves)
-    int NW, HM, MAXR, NMW, slot, nk0, nta, n_stages, nbias, Kl, ldf0;
+    int NW, NS, HM, MAXR, NMW, slot, nk0, nta, n_stages, nbias, Kl, ldf0;
     int r0, ns0;           // layer-0 row tiles per stage (their k-steps share one slot) and its stages
     int nrt[MARF_MAX_LAYERS], nrtb[MARF_MAX_LAYERS], boff[MARF_MAX_LAYERS];
     size_t prog_off, bias_off, kmap_off, end_off;
@@ -87,6 +87,7 @@ static void plan_step2_net(marf_net* n) {
         if (q.variant == 0 && e && e[0] == '1') q.variant = 2;
     }
     q.NW = q.variant == 0 ? 8 : 4;
+    q.NS = q.variant == 1 ? 2 : 1;  // pixel sets per dgrad pass (S2Cfg::NS)
     q.MAXR = 4;
     q.NMW = q.HM / 64;
     q.slot = (q.HM / 16) * 1024 * (q.variant == 1 ? 2 : 1);
@@ -713,12 +714,15 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
         off += rup(Ssave * p.S * (l == 0 ? q.ldf0 : n->Kp[l]) * 2, 256);
     }
     p.dz[0] = 0;
+    // dz_l and the dH partials carry 32 NW sink rows past S: the dgrad pass of a pixel set that has
+    // no tile (an odd tile count with two sets per dgrad pass) stores there
+    const long long Ssink = p.S + 32 * q.NW;
     for (int l = 1; l < nl; ++l) {
         p.dz[l] = off;
-        off += rup(Ssave * p.S * n->Kp[l] * 2, 256);
+        off += rup(Ssave * Ssink * n->Kp[l] * 2, 256);
     }
     p.dH = off;
-    off += rup(Ssave * p.S / 32 * 9 * 4, 256);
+    off += rup(Ssave * Ssink / 32 * 9 * 4, 256);
     p.loss = off;
     off += rup((long long)p.grid * 2 * 8, 256);
     p.blast = off;
@@ -769,10 +773,13 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     a.c2f_on = cf.on;
     a.prog = pk + q.prog_off;
     a.n_stages = q.n_stages;
-    if (render) {  // the program's forward prefix: the layer-0 and hidden row tiles + the last layer
+    // the program's forward prefix: the layer-0 and hidden row tiles + the last layer
+    a.n_fwd = 1 + q.ns0;
+    for (int l = 1; l < nl - 1; ++l) a.n_fwd += q.nrt[l];
+    a.S = p.S;
+    if (render) {
         a.fwd_only = 1;
-        a.n_stages = 1 + q.ns0;
-        for (int l = 1; l < nl - 1; ++l) a.n_stages += q.nrt[l];
+        a.n_stages = a.n_fwd;
         a.pro_fallback = a.geo.mode == MARF_GEO_COORDS ? a.geo.coords : a.geo.Hm;
     }
     a.bias = (const float*)(pk + q.bias_off);
@@ -811,7 +818,8 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     a.lds_layers = off;
     off += (int)sizeof(S2Layer) * MARF_MAX_LAYERS;
     a.lds_wave = off;
-    a.lds_wave_bytes = (int)rup(2048 + q.MAXR * q.NMW * 256 + 12 * q.Kl, 16);
+    // per wave: transpose + g^T scratch, ReLU mask words of each pixel set of a dgrad pass, dW_last
+    a.lds_wave_bytes = (int)rup(2048 + q.NS * q.MAXR * q.NMW * 256 + 12 * q.Kl, 16);
     off += q.NW * a.lds_wave_bytes;
     a.lds_total = off;
     if (off > 160 * 1024) return fail(MARF_ERR_UNSUPPORTED, "step2: LDS plan %d B exceeds 160 KB", off);

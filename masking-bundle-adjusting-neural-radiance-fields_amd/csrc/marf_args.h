@@ -88,13 +88,16 @@ struct Step2Args {
     int r0;                          // layer-0 row tiles per stage
     const char* prog;                // weight stage program: n_stages slots of SLOT bytes
     int n_stages;
+    int n_fwd;                       // the program's forward stages (the first n_fwd; the rest: dgrad)
+    long long S;                     // pixel slots; rows S .. S + 32 NW - 1 of dz_l / dH: store sink
+                                     // of a backward pixel set that has no tile (odd tile count)
     const float* bias;               // padded biases
     int nbias;                       // floats in the bias table
     const float* gt;                 // [B][3][Np]
     const float* mask;               // [B][1][Np] or null
     float* rgb;                      // [B][Np][3] or null
     S2Layer layers[MARF_MAX_LAYERS]; // per-layer table (copied into LDS at kernel start)
-    float* dH_partial;               // [S / 32][9]
+    float* dH_partial;               // [S / 32 + NW][9]
     double* loss_partial;            // [grid][2]
     float* blast_partial;            // [grid][3]
     float* wlast_partial;            // [grid][3][Kl]

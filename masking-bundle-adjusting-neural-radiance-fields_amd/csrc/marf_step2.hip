@@ -34,14 +34,6 @@ namespace marf {
 
 // ------------------------------------------------------------------ inline-asm memory ops
 
-// LDS-DMA, 16 B per lane (1 KB per wave instruction), lds = wave-uniform LDS byte address
-MARF_DEV void s2_glds16(const void* src, unsigned lds) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(src), "s"(lds)
-                 : "memory");
-}
 // LDS-DMA, 4 B per lane (256 B per wave instruction)
 MARF_DEV void s2_glds4(const void* src, unsigned lds) {
     unsigned keep;
@@ -149,18 +141,22 @@ struct S2Cfg {
     static constexpr int LO = NKH * 1024;                  // byte offset of the lo fragments in a slot
     static constexpr int PER_DMA = SLOT / (NW * 1024);     // DMA instructions per wave per stage
     static constexpr int NSLOT = 3, D = 2;
-    static constexpr int ST = 2;                           // store instructions per wave per stage
+    // pixel sets (tiles) whose dgrad shares each weight stage: the split recipe's dgrad operands are
+    // bf16 hi only, so at one wave per SIMD two 32-pixel sets fit the register file there (the
+    // forward's hi + lo activations do not); the 8-wave plain variant has 256 registers per wave
+    static constexpr int NS = SPLIT ? 2 : 1;
     static constexpr int NK0 = 9;                          // max layer-0 k-steps (L <= 32)
     static constexpr int NTA = 5;                          // max adjoint row tiles (L <= 39)
     static constexpr int TPX = 32 * NW;                    // pixel slots per block tile
     static constexpr int NMW = NRT / 2;                    // mask words per ReLU layer
+    static constexpr int MSET = MAXR * NMW * 64;           // mask words of one pixel set (per wave)
     static_assert(PER_DMA * NW * 1024 == SLOT, "slot size");
 };
 
 template <int HM, bool SPLIT, int NW, int MAXR>
 __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     typedef S2Cfg<HM, SPLIT, NW, MAXR> C;
-    constexpr int NKH = C::NKH, NRT = C::NRT, ST = C::ST;
+    constexpr int NKH = C::NKH, NRT = C::NRT, NS = C::NS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -183,9 +179,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     char* wpriv = smem + a.lds_wave + wave * a.lds_wave_bytes;
     u16* trs = reinterpret_cast<u16*>(wpriv);                 // 1 KB transpose scratch
     u16* gts = reinterpret_cast<u16*>(wpriv + 1024);          // 1 KB g^T image [16][32]
-    uint32_t* mkl = reinterpret_cast<uint32_t*>(wpriv + 2048);  // ReLU mask words [MAXR][NMW][64]
-    float* wla = reinterpret_cast<float*>(wpriv + 2048 + MAXR * C::NMW * 256);  // [3][Kl] dW_last
-    float* dmy = a.dummy + (((size_t)blockIdx.x * NW + wave) * ST * 64 + lane) * 2;
+    uint32_t* mkl = reinterpret_cast<uint32_t*>(wpriv + 2048);  // ReLU mask words [NS][MAXR][NMW][64]
+    float* wla = reinterpret_cast<float*>(wpriv + 2048 + NS * C::MSET * 4);  // [3][Kl] dW_last
+    float* dmy = a.dummy + (((size_t)blockIdx.x * NW + wave) * 2 * 64 + lane) * 2;
 #ifdef MARF_STAMPS
     unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -202,7 +198,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     const int Np = a.geo.Np;
     int my_tiles = 0;
     if ((int)blockIdx.x < a.n_tiles) my_tiles = (a.n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
-    const int total = my_tiles * a.n_stages;
+    // Stage order of a group of NS tiles: the forward stages of each tile, then ONE pass of the
+    // dgrad stages for all of them (render: forward stages only)
+    const int nF = a.n_fwd, nB = a.n_stages - a.n_fwd;
+    const int total = (my_tiles / NS) * (NS * nF + nB) + (my_tiles % NS ? (my_tiles % NS) * nF + nB : 0);
 
     // ---- per-tile input DMA: target r, g, b, mask (TPX floats each) and H (9 floats) of a tile
     auto pro_buf = [&](int pb) -> float* { return reinterpret_cast<float*>(smem + a.lds_pro + pb * (4 * C::TPX + 64) * 4); };
@@ -226,53 +225,77 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     // ---- the weight ring
     int c_stage = 0;         // global stage counter of this block
     int dma_stage = 0;       // next stage whose DMA is to be issued
-    int dma_prog = 0;        // its index in the program
-    auto issue_stage = [&]() {
-        const unsigned dst = lds0 + (dma_stage % C::NSLOT) * C::SLOT;
-        const char* src = a.prog + (size_t)dma_prog * C::SLOT;
-#pragma unroll
-        for (int i = 0; i < C::PER_DMA; ++i) {
-            const int piece = wave * C::PER_DMA + i;
-            s2_glds16(src + piece * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(dst + piece * 1024));
-        }
-        ++dma_stage;
-        if (++dma_prog == a.n_stages) dma_prog = 0;
+    // DMA cursor over the group sequence: index in the group, its length, its tile count, first tile
+    int dg_i = 0, dg_n = 0, dg_ns = 0, dg_t = 0;
+    auto grp_init = [&](int t) {
+        dg_t = t;
+        dg_ns = min(NS, my_tiles - t);
+        dg_n = dg_ns * nF + nB;
+        dg_i = 0;
     };
-    // The refill of the slot freed at a stage's barrier is issued piece by piece beside the stage's
-    // MFMAs (dma_piece from the GEMM loop), the rest before the stage's first store (dma_flush):
-    // LDS-DMA issue is throttled by the CU's L2 -> LDS rate, so a burst would stall the wave.
-    int dma_left = 0;
-    unsigned dma_dst = 0;
-    const char* dma_src = nullptr;
+    grp_init(0);
+    auto dma_next = [&]() -> int {  // program stage of the next DMA; the cursor advances
+        const int i = dg_i;
+        const int prog = i < nF ? i : (i < dg_ns * nF ? i - nF : i - (dg_ns - 1) * nF);
+        if (++dg_i == dg_n) grp_init(dg_t + NS);
+        return prog;
+    };
+    // The refill of the slot freed at a stage's barrier: PER_DMA pieces of 1 KB per wave, every
+    // stage exactly once, all of them before the stage's first store.  Regular stages (one 16-k-step
+    // GEMM per pixel set) issue them beside the MFMAs of the first GEMM (dma_piece<j> at fixed
+    // k-steps); the others (layer 0, the last-layer dgrad) issue them right after the barrier.  A
+    // piece is branch-free: m0 = the stage's LDS base, the VGPR address the stage's source, and the
+    // instruction offset (j mod 4) KB moves both (the second half of the pieces from bases 4 KB on).
+    // Past the last stage the ring refills the just-freed slot from program stage 0 (never read).
+    unsigned dma_m0 = 0;
+    const char* dma_va0 = nullptr;
+    const char* dma_va1 = nullptr;
     auto dma_arm = [&]() {
-#ifdef S2_DIAG_NODMA
+        const int ps = dma_stage < total ? dma_next() : 0;
+        dma_m0 = __builtin_amdgcn_readfirstlane(lds0 + (dma_stage % C::NSLOT) * C::SLOT + wave * C::PER_DMA * 1024);
+        dma_va0 = a.prog + (size_t)ps * C::SLOT + wave * C::PER_DMA * 1024 + lane * 16;
+        if constexpr (C::PER_DMA > 4) dma_va1 = dma_va0 + 4096;
         ++dma_stage;
-        if (++dma_prog == a.n_stages) dma_prog = 0;
-        return;
+    };
+    auto dma_piece = [&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        static_assert(j < C::PER_DMA && C::PER_DMA <= 8, "piece index");
+        const char* va = j < 4 ? dma_va0 : dma_va1;
+        const unsigned m = dma_m0 + (j < 4 ? 0u : 4096u);
+#ifndef S2_DIAG_NODMA
+        unsigned keep;  // m0 is reserved to the compiler: saved and restored around the piece
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off offset:%3\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(va), "s"(m), "n"((j & 3) * 1024)
+                     : "memory");
+#else
+        (void)va;
+        (void)m;
 #endif
-        dma_dst = lds0 + (dma_stage % C::NSLOT) * C::SLOT + wave * C::PER_DMA * 1024;
-        dma_src = a.prog + (size_t)dma_prog * C::SLOT + wave * C::PER_DMA * 1024 + lane * 16;
-        dma_left = C::PER_DMA;
-        ++dma_stage;
-        if (++dma_prog == a.n_stages) dma_prog = 0;
     };
-    auto dma_piece = [&]() {
-        if (dma_left > 0) {
-            s2_glds16(dma_src, __builtin_amdgcn_readfirstlane(dma_dst));
-            dma_src += 1024;
-            dma_dst += 1024;
-            --dma_left;
-        }
+    auto dma_burst = [&]() { s2_sfor<C::PER_DMA>([&](auto jc) { dma_piece(jc); }); };
+    // vm-op accounting for the ring waits: st_cur counts the store instructions a wave issued since
+    // the last stage_begin (all of them after that stage's DMA pieces), st_prev the count of the
+    // stage before.  The DMA of stage c was issued during stage c-2, so st_prev + PER_DMA (the
+    // pieces of stage c+1) + st_cur operations are younger than it: vmcnt(that) waits for it (any
+    // smaller count is a stricter wait; the operations complete in order).
+    int st_cur = 0, st_prev = 0;
+    auto wait_ring = [&]() {
+        const int y = st_prev + st_cur;
+        constexpr int PD = C::PER_DMA;
+        if (y >= 8) s2_wait_vm<PD + 8>();
+        else if (y >= 6) s2_wait_vm<PD + 6>();
+        else if (y >= 4) s2_wait_vm<PD + 4>();
+        else if (y >= 2) s2_wait_vm<PD + 2>();
+        else s2_wait_vm<PD>();
     };
-    auto dma_flush = [&]() {
-        while (dma_left > 0) dma_piece();
-    };
-    // wait for stage c_stage, publish it to every wave, refill the slot freed by stage c_stage - 1
-    auto stage_begin = [&]() -> const char* {
-        dma_flush();
+    // wait for stage c_stage, publish it to every wave, arm the refill of the slot freed by stage
+    // c_stage - 1 (burst: issue it now)
+    auto stage_begin = [&](bool burst) -> const char* {
         S2T_BEGIN(0);
-        if (c_stage + 1 < total) s2_wait_vm<C::D * ST + C::PER_DMA>();
-        else s2_wait_vm<C::D * ST>();
+        wait_ring();
+        st_prev = st_cur;
+        st_cur = 0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #ifndef S2_DIAG_NOBAR  // (S2_DIAG_* : timing-only diagnostic builds, results invalid)
         __builtin_amdgcn_s_barrier();
@@ -280,7 +303,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         asm volatile("" ::: "memory");
         S2T_END(0);
         S2T_BEGIN(1);
-        if (dma_stage < total) dma_arm();
+        dma_arm();
+        if (burst) dma_burst();
         S2T_END(1);
         const char* slot = smem + (c_stage % C::NSLOT) * C::SLOT;
         ++c_stage;
@@ -289,8 +313,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
 
     if (my_tiles > 0) {
         issue_pro((int)blockIdx.x, 0);
-        if (dma_stage < total) issue_stage();
-        if (dma_stage < total) issue_stage();
+        dma_arm();
+        dma_burst();
+        dma_arm();
+        dma_burst();
     }
     s2_wait_vm<0>();
     __syncthreads();
@@ -299,27 +325,18 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     double lsq = 0.0, lms = 0.0;
     float bl0 = 0.f, bl1 = 0.f, bl2 = 0.f;
 
-    // ReLU mask words in wave-private LDS: word (layer, rt >> 1) of a lane, bit
+    // ReLU mask words in wave-private LDS: word (set, layer, rt >> 1) of a lane, bit
     // (16 (1 - (rt & 1)) + 15 - r) = accumulator register r (the pair of row tiles is assembled in
     // a register, so each word is written once)
     uint32_t mpend = 0u;
 
     S2Frag Bh[NKH], Bl[NKH], Oh[NKH], Ol[NKH];
 
-    auto dummies = [&](auto n_tag) {
-        constexpr int N = decltype(n_tag)::value;
-        dma_flush();
-#pragma unroll
-        for (int i = 0; i < N; ++i) s2_st8(dmy + i * 128, 0u, 0u);
-    };
-    typedef std::integral_constant<int, ST> STt;
-    typedef std::integral_constant<int, ST - 1> ST1t;
     // (the stores of a row tile into a natural-order [S][ld] bf16 tensor: k-step ks of the lane's
     //  pixel holds columns 16 ks + 4 h + 0..3 (dwords x, y) and 16 ks + 8 + 4 h + 0..3 (z, w); two
     //  v_permlane32_swap exchange the lane halves' x, y <-> z, w so that lane (p, h) holds columns
     //  16 ks + 8 h + 0..7 contiguously: one 16-B store per lane per k-step, 2 per row tile)
     auto store_rt = [&](u16* base, int ld, long long slot, int rt, const S2Frag& f0, const S2Frag& f1) {
-        dma_flush();
         u16* row = base + slot * ld + 32 * rt + 8 * h;
         auto contig = [&](const S2Frag& f) -> uint4 {
             const auto xz = __builtin_amdgcn_permlane32_swap(f.u.x, f.u.z, false, false);
@@ -328,8 +345,36 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         };
         s2_st16(row, contig(f0));
         s2_st16(row + 16, contig(f1));
+        st_cur += 2;
     };
 
+    // one 32-row output tile: acc (+)= A[ks] . B[ks] over NK k-steps from the slot
+    //   MODE 0: plain; 1: split forward (hi.hi + hi.lo + lo.hi)
+    // With one wave per SIMD the issue is in order, so the filler work of a k-step goes INTO the
+    // gaps between its MFMAs (each gap hides ~24 cycles of issue): hook(ks, 0) after the first
+    // MFMA, hook(ks, 1) after the second (right after the first in plain mode), the A-ring refill
+    // of each register right after the last MFMA that reads it, the DMA piece after the last MFMA.
+    // sched_barrier pins that order (left alone the scheduler sinks each LDS read to right before
+    // its MFMA, exposing its latency, and bunches the VALU behind the MFMA chain).
+    auto nohook = [&](auto, auto) {};
+    // the stage's DMA pieces beside the MFMAs of a 16-k-step GEMM: piece j after k-step
+    // (j + 1) NK / PER_DMA - 1 (PIECES: this GEMM is its stage's first)
+    auto piece_at = [&](auto ksc, auto nk_tag, auto pieces_tag) {
+        constexpr int ks = decltype(ksc)::value;
+        constexpr int NK = decltype(nk_tag)::value;
+        if constexpr (decltype(pieces_tag)::value) {
+            static_assert(NK % C::PER_DMA == 0, "pieces per k-step");
+            constexpr int per = NK / C::PER_DMA;
+            if constexpr (ks % per == per - 1) dma_piece(std::integral_constant<int, ks / per>());
+        }
+    };
+    typedef std::integral_constant<bool, true> PcOn;    // the GEMM issues its stage's DMA pieces
+    typedef std::integral_constant<bool, false> PcOff;
+    // one accumulation chain (a second, alternating accumulator measured no faster, and any change
+    // of the summation order re-rolls the seed-3 basin: DESIGN.md §4)
+    auto mf = [&](f32x16& acc, const bf16x8& x, const bf16x8& y) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc, 0, 0, 0);
+    };
     // one 32-row output tile: acc (+)= A[ks] . B[ks] over NK k-steps from the slot
     //   MODE 0: plain; 1: split forward (hi.hi + hi.lo + lo.hi); 2: split dgrad (hi.B + lo.B)
     // With one wave per SIMD the issue is in order, so the filler work of a k-step goes INTO the
@@ -338,9 +383,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     // of each register right after the last MFMA that reads it, the DMA piece after the last MFMA.
     // sched_barrier pins that order (left alone the scheduler sinks each LDS read to right before
     // its MFMA, exposing its latency, and bunches the VALU behind the MFMA chain).
-    auto nohook = [&](auto, auto) {};
     auto gemm = [&](f32x16& acc, const char* slot, const S2Frag* Bhi, const S2Frag* Blo, int nk, auto mode_tag,
-                    auto nk_tag, auto&& hook) {
+                    auto nk_tag, auto&& hook, auto pieces_tag) {
         constexpr int MODE = decltype(mode_tag)::value;
         constexpr int NK = decltype(nk_tag)::value;
         typedef std::integral_constant<int, 0> P0;
@@ -357,28 +401,17 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         s2_sfor<NK>([&](auto ksc) {
             constexpr int ks = decltype(ksc)::value;
             constexpr int u = ks & 3;
+#ifdef S2_DIAG_NOALDS  // timing only: the A fragments are not refilled from LDS (results invalid)
+            constexpr bool refill = false;
+#else
             constexpr bool refill = ks + P < NK;
+#endif
             const bool live = NK != C::NK0 || ks < nk;
-            auto piece = [&]() {
-                if constexpr (NK >= 2 * C::PER_DMA) {
-                    if constexpr ((ks & 1) == 1) dma_piece();
-                } else {
-                    dma_piece();
-                }
-            };
-            // one accumulation chain (a second, alternating accumulator measured no faster, and
-            // any change of the summation order re-rolls the seed-3 basin: DESIGN.md §4)
-            auto mf = [&](auto, const bf16x8& x, const bf16x8& y) {
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc, 0, 0, 0);
-            };
-            constexpr int PER = MODE == 0 ? 1 : (MODE == 1 ? 3 : 2);
-            typedef std::integral_constant<int, PER * ks> J0;
-            typedef std::integral_constant<int, PER * ks + 1> J1;
-            typedef std::integral_constant<int, PER * ks + 2> J2;
+            auto piece = [&]() { piece_at(ksc, nk_tag, pieces_tag); };
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (MODE == 0) {
                 if (live) {
-                    mf(J0(), A0[u], Bhi[ks].f);
+                    mf(acc, A0[u], Bhi[ks].f);
                     hook(ksc, P0());
                     hook(ksc, P1());
                 }
@@ -386,14 +419,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 if (live) piece();
             } else if constexpr (MODE == 2) {
                 if (live) {
-                    mf(J0(), A0[u], Bhi[ks].f);
+                    mf(acc, A0[u], Bhi[ks].f);
                     hook(ksc, P0());
                 }
                 if constexpr (refill) A0[u] = ah[(ks + P) * 64];
                 __builtin_amdgcn_sched_barrier(0);
                 if (live) {
 #ifndef S2_BWD_NO_W_LO  // numerics experiment: dgrad with W_hi^T only
-                    mf(J1(), A1[u], Bhi[ks].f);
+                    mf(acc, A1[u], Bhi[ks].f);
 #endif
                     hook(ksc, P1());
                 }
@@ -401,20 +434,20 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 if (live) piece();
             } else {
                 if (live) {
-                    mf(J0(), A0[u], Bhi[ks].f);
+                    mf(acc, A0[u], Bhi[ks].f);
                     hook(ksc, P0());
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (live) {
 #ifndef S2_FWD_NO_ACT_LO  // numerics experiment: activations carried as bf16 hi only
-                    mf(J1(), A0[u], Blo[ks].f);
+                    mf(acc, A0[u], Blo[ks].f);
 #endif
                     hook(ksc, P1());
                 }
                 if constexpr (refill) A0[u] = ah[(ks + P) * 64];
                 __builtin_amdgcn_sched_barrier(0);
 #ifndef S2_FWD_NO_W_LO  // numerics experiment: forward weights bf16 hi only
-                if (live) mf(J2(), A1[u], Bhi[ks].f);
+                if (live) mf(acc, A1[u], Bhi[ks].f);
 #endif
                 if constexpr (refill) A1[u] = al[(ks + P) * 64];
                 if (live) piece();
@@ -422,7 +455,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             __builtin_amdgcn_sched_barrier(0);
         });
     };
-    typedef std::integral_constant<int, 0> M0t;
     typedef std::integral_constant<int, SPLIT ? 1 : 0> MFt;
     typedef std::integral_constant<int, SPLIT ? 2 : 0> MBt;
     typedef std::integral_constant<int, NKH> NKHt;
@@ -509,8 +541,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         frelu(pa, ec);
         fpack(ec);
     };
-    // forward finish of tile rt: operand fragments of k-steps 2 rt, 2 rt + 1, mask word, 4 stores
-    auto ffinish = [&](int l, auto rtc, bool save, u16* sbase, int sld) {
+    // forward finish of tile rt: operand fragments of k-steps 2 rt, 2 rt + 1, mask word, 2 stores
+    auto ffinish = [&](int l, auto rtc, bool save, u16* sbase, int sld, uint32_t* mks) {
         constexpr int rt = decltype(rtc)::value;
 #ifdef S2_DIAG_NOEPI
         return;
@@ -522,12 +554,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             Ol[2 * rt + 1].u = make_uint4(ep.lw[4], ep.lw[5], ep.lw[6], ep.lw[7]);
         }
         if constexpr ((rt & 1) == 0) mpend = ep.bits << 16;
-        else mkl[(l * C::NMW + (rt >> 1)) * 64 + lane] = mpend | ep.bits;
+        else mks[(l * C::NMW + (rt >> 1)) * 64 + lane] = mpend | ep.bits;
         if (save) store_rt(sbase, sld, myslot_g, rt, Oh[2 * rt], Oh[2 * rt + 1]);
-        else dummies(std::integral_constant<int, ST>());
     };
-    // dgrad step e: dz = acc * relu'(z) with the mask word ep.mw
-    auto bstep = [&](const f32x16& pa, auto ec, auto rtc) {
+    // dgrad step e: dz = acc * relu'(z) with the mask word e.mw
+    auto bstep = [&](EpSt& es, const f32x16& pa, auto ec, auto rtc) {
         constexpr int e = decltype(ec)::value;
 #ifdef S2_DIAG_NOEPI
         return;
@@ -539,295 +570,367 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             "v_bfe_i32 %0, %1, %3, 1\n\t"
             "v_and_b32_e32 %0, %0, %2"
             : "=&v"(x)
-            : "v"(ep.mw), "v"(pa[e]), "n"(bit));
+            : "v"(es.mw), "v"(pa[e]), "n"(bit));
         if constexpr (e & 1) {
             uint32_t w;
-            asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(ep.vp), "v"(x));
-            ep.hw[e >> 1] = w;
+            asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(es.vp), "v"(x));
+            es.hw[e >> 1] = w;
         } else {
-            ep.vp = x;
+            es.vp = x;
         }
     };
-    auto bfinish = [&](auto rtc, u16* sbase, int sld) {
+    auto bfinish = [&](EpSt& es, S2Frag* O, auto rtc, u16* sbase, int sld, long long slot) {
         constexpr int rt = decltype(rtc)::value;
 #ifdef S2_DIAG_NOEPI
         return;
 #endif
-        Oh[2 * rt].u = make_uint4(ep.hw[0], ep.hw[1], ep.hw[2], ep.hw[3]);
-        Oh[2 * rt + 1].u = make_uint4(ep.hw[4], ep.hw[5], ep.hw[6], ep.hw[7]);
-        store_rt(sbase, sld, myslot_g, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+        O[2 * rt].u = make_uint4(es.hw[0], es.hw[1], es.hw[2], es.hw[3]);
+        O[2 * rt + 1].u = make_uint4(es.hw[4], es.hw[5], es.hw[6], es.hw[7]);
+        store_rt(sbase, sld, slot, rt, O[2 * rt], O[2 * rt + 1]);
     };
     const float pi_f = 3.14159265358979323846f;
 
-    S2T_BEGIN(7);
-    for (int it = 0; it < my_tiles; ++it) {
-        S2T_BEGIN(4);
-        const int tile = (int)blockIdx.x + it * (int)gridDim.x;
-        const int pb = it & 1;
-        const int b = tile / tpp;
-        const int p0 = (tile - b * tpp) * C::TPX + 32 * wave;
-        const long long slot0 = (long long)b * a.geo.Np_pad + p0;
-        const long long myslot = slot0 + pxl;
-        myslot_g = myslot;
-        const int p = p0 + pxl;
-        const bool valid = p < Np;
-        const float* pro = pro_buf(pb);
+    // what the dgrad pass keeps of each pixel set's forward: the g operand, the warp's homogeneous
+    // point and the tile (-1: no tile; the set's stores go to the sink rows); the rest is recomputed
+    struct SetSt {
+        S2Frag g;
+        float X0, X1, X2;
+        int tile;
+    };
+    SetSt ss[NS];
 
-        // ---- prologue: pixel grid -> warp (warp.py:33-81) -> posenc + c2f features (model/planar.py:451-471)
-        float Hm[9];
+    S2T_BEGIN(7);
+    for (int it = 0; it < my_tiles; it += NS) {
+        const int nset = min(NS, my_tiles - it);
+        for (int si = 0; si < nset; ++si) {
+            S2T_BEGIN(4);
+            const int ti = it + si;
+            const int tile = (int)blockIdx.x + ti * (int)gridDim.x;
+            const int pb = ti & 1;
+            const int b = tile / tpp;
+            const int p0 = (tile - b * tpp) * C::TPX + 32 * wave;
+            const long long slot0 = (long long)b * a.geo.Np_pad + p0;
+            const long long myslot = slot0 + pxl;
+            myslot_g = myslot;
+            const int p = p0 + pxl;
+            const bool valid = p < Np;
+            const float* pro = pro_buf(pb);
+            uint32_t* mks = mkl + si * C::MSET;
+
+            // ---- prologue: pixel grid -> warp (warp.py:33-81) -> posenc + c2f features (model/planar.py:451-471)
+            float Hm[9];
 #pragma unroll
-        for (int e = 0; e < 9; ++e) Hm[e] = pro[4 * C::TPX + e];
-        float x, y, u, v, X[3];
-        if (a.geo.mode == 1) {  // explicit coordinates (GeoDev mode 1; render only)
-            const int pc = min(p, Np - 1);
-            u = x = a.geo.coords[2 * (size_t)pc];
-            v = y = a.geo.coords[2 * (size_t)pc + 1];
-            X[0] = u;
-            X[1] = v;
-            X[2] = 1.0f;
-        } else {
-            const int r = p / a.geo.w, cc = p - r * a.geo.w;
-            x = grid_coord(a.geo.x0 + cc, a.geo.W, a.geo.norm_w);
-            y = grid_coord(a.geo.y0 + r, a.geo.H, a.geo.norm_h);
-            warp_point(Hm, x, y, u, v, X, a.geo.bmm_small);
-        }
-        const float cd = h ? v : u;
-        S2Frag F0h[C::NK0], F0l[C::NK0];
-        {
-            const int ng = a.nk0 - 1;  // band groups of 4
-#pragma unroll
-            for (int g = 0; g < C::NK0 - 1; ++g) {
-                if (g < ng) {
-                    float f[8];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int k = 4 * g + j;
-                        float s = 0.f, co = 0.f;
-                        if (k < L) {
-                            band_sincos<true>(cd, k, s, co);
-                            if (a.c2f_on) {
-                                const float w = c2f_l[k];
-                                s = s * w;
-                                co = co * w;
-                            }
-                        }
-                        f[j] = s;
-                        f[4 + j] = co;
-                    }
-                    s2_split8<SPLIT>(f, F0h[g], F0l[g]);
-                }
+            for (int e = 0; e < 9; ++e) Hm[e] = pro[4 * C::TPX + e];
+            float x, y, u, v, X[3];
+            if (a.geo.mode == 1) {  // explicit coordinates (GeoDev mode 1; render only)
+                const int pc = min(p, Np - 1);
+                u = x = a.geo.coords[2 * (size_t)pc];
+                v = y = a.geo.coords[2 * (size_t)pc + 1];
+                X[0] = u;
+                X[1] = v;
+                X[2] = 1.0f;
+            } else {
+                const int r = p / a.geo.w, cc = p - r * a.geo.w;
+                x = grid_coord(a.geo.x0 + cc, a.geo.W, a.geo.norm_w);
+                y = grid_coord(a.geo.y0 + r, a.geo.H, a.geo.norm_h);
+                warp_point(Hm, x, y, u, v, X, a.geo.bmm_small);
             }
-            float f[8] = {cd, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            S2Frag rh, rl;
-            s2_split8<SPLIT>(f, rh, rl);
+            const float cd = h ? v : u;
+            S2Frag F0h[C::NK0], F0l[C::NK0];
+            {
+                const int ng = a.nk0 - 1;  // band groups of 4
 #pragma unroll
-            for (int g = 0; g < C::NK0; ++g)
-                if (g == ng) {
-                    F0h[g] = rh;
-                    F0l[g] = rl;
+                for (int g = 0; g < C::NK0 - 1; ++g) {
+                    if (g < ng) {
+                        float f[8];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int k = 4 * g + j;
+                            float s = 0.f, co = 0.f;
+                            if (k < L) {
+                                band_sincos<true>(cd, k, s, co);
+                                if (a.c2f_on) {
+                                    const float w = c2f_l[k];
+                                    s = s * w;
+                                    co = co * w;
+                                }
+                            }
+                            f[j] = s;
+                            f[4 + j] = co;
+                        }
+                        s2_split8<SPLIT>(f, F0h[g], F0l[g]);
+                    }
                 }
-            // feat_0 (bf16 hi) for the layer-0 weight gradient: column 16 ks + 8 h + j
-            if (!a.fwd_only) {
-                u16* row = ly_ptr(0, 0) + myslot * ly_int(0, 3);
+                float f[8] = {cd, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                S2Frag rh, rl;
+                s2_split8<SPLIT>(f, rh, rl);
 #pragma unroll
                 for (int g = 0; g < C::NK0; ++g)
-                    if (g < a.nk0) s2_st16(row + 16 * g + 8 * h, F0h[g].u);
-                if (16 * a.nk0 < ly_int(0, 3)) s2_st16(row + 16 * a.nk0 + 8 * h, make_uint4(0, 0, 0, 0));
+                    if (g == ng) {
+                        F0h[g] = rh;
+                        F0l[g] = rl;
+                    }
+                // feat_0 (bf16 hi) for the layer-0 weight gradient: column 16 ks + 8 h + j
+                // (every armed DMA piece was issued before the previous store: these count as the
+                //  current stage's stores)
+                if (!a.fwd_only) {
+                    u16* row = ly_ptr(0, 0) + myslot * ly_int(0, 3);
+#pragma unroll
+                    for (int g = 0; g < C::NK0; ++g)
+                        if (g < a.nk0) s2_st16(row + 16 * g + 8 * h, F0h[g].u);
+                    st_cur += a.nk0;
+                    if (16 * a.nk0 < ly_int(0, 3)) {
+                        s2_st16(row + 16 * a.nk0 + 8 * h, make_uint4(0, 0, 0, 0));
+                        st_cur += 1;
+                    }
+                }
             }
-        }
 
-        S2T_END(4);
-        S2T_BEGIN(5);
-        // ---- forward, layer 0 then the hidden layers: one stage per 32-row output tile; the
-        //      epilogue of tile rt-1 (ReLU, mask bits, bf16 split, stores) runs beside the MFMAs
-        //      of tile rt, the last tile's epilogue right after its own MFMAs
-        auto fwd_layer = [&](int l, const S2Frag* Bhi, const S2Frag* Blo, int nk, auto nk_tag, auto ms_tag) {
-            constexpr int MS = decltype(ms_tag)::value;  // epilogue micro-steps beside each k-step
-            const int nrt = ly_int(l, 0);
-            const bool save = l + 1 < nl - 1 && !a.fwd_only;
-            u16* sbase = save ? ly_ptr(l + 1, 0) : nullptr;
-            const int sld = save ? ly_int(l + 1, 3) : 0;
-            const int boff = ly_int(l, 2);
-            const char* slot0 = nullptr;
-            s2_sfor<NRT>([&](auto rtc) {
-                constexpr int rt = decltype(rtc)::value;
-                f32x16& cur = (rt & 1) ? acc1 : acc0;
-                f32x16& prv = (rt & 1) ? acc0 : acc1;
-                if (rt < nrt) {
-                    // layer 0: r0 row tiles share a stage (their few k-steps fill one slot)
-                    const int sub = l == 0 ? rt % a.r0 : 0;
-                    if (sub == 0) slot0 = stage_begin();
-                    const char* slot = slot0 + sub * a.nk0 * 1024;
-                    // the next tile's target / mask / H into the other input buffer (the tile that
-                    // read it last finished before this stage's barrier)
-                    if (l == 0 && rt == 0 && it + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
-                    cur = bias_init(boff, rt);
-                    if constexpr (rt == 0) {
-                        gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, nohook);
-                        dummies(STt());
-                    } else {
-                        ep.bits = 0;
-                        gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, [&](auto ksc, auto pc) {
-                            s2_sfor<MS>([&](auto jc) {
-                                constexpr int e = decltype(ksc)::value * MS + decltype(jc)::value;
-                                if constexpr (e < 16) {
-                                    if constexpr (decltype(pc)::value == 0) frelu(prv, std::integral_constant<int, e>());
-                                    else fpack(std::integral_constant<int, e>());
-                                }
+            S2T_END(4);
+            S2T_BEGIN(5);
+            // ---- forward, layer 0 then the hidden layers: one stage per 32-row output tile; the
+            //      epilogue of tile rt-1 (ReLU, mask bits, bf16 split, stores) runs beside the MFMAs
+            //      of tile rt, the last tile's epilogue right after its own MFMAs
+            auto fwd_layer = [&](int l, const S2Frag* Bhi, const S2Frag* Blo, int nk, auto nk_tag, auto ms_tag) {
+                constexpr int MS = decltype(ms_tag)::value;  // epilogue micro-steps beside each k-step
+                typedef std::integral_constant<bool, decltype(nk_tag)::value == NKH> PcL;  // hidden: pieces in the GEMM
+                const int nrt = ly_int(l, 0);
+                const bool save = l + 1 < nl - 1 && !a.fwd_only;
+                u16* sbase = save ? ly_ptr(l + 1, 0) : nullptr;
+                const int sld = save ? ly_int(l + 1, 3) : 0;
+                const int boff = ly_int(l, 2);
+                const char* slot0 = nullptr;
+                s2_sfor<NRT>([&](auto rtc) {
+                    constexpr int rt = decltype(rtc)::value;
+                    f32x16& cur = (rt & 1) ? acc1 : acc0;
+                    f32x16& prv = (rt & 1) ? acc0 : acc1;
+                    if (rt < nrt) {
+                        // layer 0: r0 row tiles share a stage (their few k-steps fill one slot)
+                        const int sub = l == 0 ? rt % a.r0 : 0;
+                        if (sub == 0) slot0 = stage_begin(l == 0);  // layer 0: the pieces in a burst
+                        const char* slot = slot0 + sub * a.nk0 * 1024;
+                        // the next tile's target / mask / H into the other input buffer (the tile that
+                        // read it last finished before this stage's barrier)
+                        if (l == 0 && rt == 0 && ti + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
+                        cur = bias_init(boff, rt);
+                        if constexpr (rt == 0) {
+                            gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, nohook, PcL());
+                        } else {
+                            ep.bits = 0;
+                            gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, [&](auto ksc, auto pc) {
+                                s2_sfor<MS>([&](auto jc) {
+                                    constexpr int e = decltype(ksc)::value * MS + decltype(jc)::value;
+                                    if constexpr (e < 16) {
+                                        if constexpr (decltype(pc)::value == 0) frelu(prv, std::integral_constant<int, e>());
+                                        else fpack(std::integral_constant<int, e>());
+                                    }
+                                });
+                            }, PcL());
+                            s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
+                                if (decltype(ec)::value >= MS * nk) fstep(prv, ec);
                             });
-                        });
-                        s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
-                            if (decltype(ec)::value >= MS * nk) fstep(prv, ec);
-                        });
-                        ffinish(l, std::integral_constant<int, rt - 1>(), save, sbase, sld);
+                            ffinish(l, std::integral_constant<int, rt - 1>(), save, sbase, sld, mks);
+                        }
+                        if (rt == nrt - 1) {
+                            ep.bits = 0;
+                            s2_sfor<16>([&](auto ec) { fstep(cur, ec); });
+                            ffinish(l, rtc, save, sbase, sld, mks);
+                        }
+                    } else {
+                        zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
                     }
-                    if (rt == nrt - 1) {
-                        ep.bits = 0;
-                        s2_sfor<16>([&](auto ec) { fstep(cur, ec); });
-                        ffinish(l, rtc, save, sbase, sld);
-                    }
-                } else {
-                    zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
-                }
-            });
+                });
 #pragma unroll
-            for (int k = 0; k < NKH; ++k) {
-                Bh[k] = Oh[k];
-                if constexpr (SPLIT) Bl[k] = Ol[k];
-            }
-        };
-        fwd_layer(0, F0h, F0l, a.nk0, NK0t(), std::integral_constant<int, 2>());
-        for (int l = 1; l < nl - 1; ++l) fwd_layer(l, Bh, Bl, NKH, NKHt(), std::integral_constant<int, 1>());
+                for (int k = 0; k < NKH; ++k) {
+                    Bh[k] = Oh[k];
+                    if constexpr (SPLIT) Bl[k] = Ol[k];
+                }
+            };
+            fwd_layer(0, F0h, F0l, a.nk0, NK0t(), std::integral_constant<int, 2>());
+            for (int l = 1; l < nl - 1; ++l) fwd_layer(l, Bh, Bl, NKH, NKHt(), std::integral_constant<int, 1>());
 
-        S2T_END(5);
-        S2T_BEGIN(6);
-        // ---- last layer: 3 outputs (rows 0..2 of one tile), sigmoid, masked MSE, d rgb
-        float g[3] = {0.f, 0.f, 0.f};
-        {
-            const char* slot = stage_begin();
-            f32x16 acc = bias_init(ly_int(nl - 1, 2), 0);
-            gemm(acc, slot, Bh, Bl, NKH, MFt(), NKHt(), nohook);
-            float* o = (a.rgb && valid && h == 0) ? a.rgb + ((size_t)b * Np + p) * 3 : dmy;
-            float yv[3] = {0.f, 0.f, 0.f};
-            if (h == 0) {
-                const float m = valid ? (a.mask ? pro[3 * C::TPX + 32 * wave + pxl] : 1.0f) : 0.f;
-                double sq = 0.0;
-                float sqf = 0.f;
+            S2T_END(5);
+            S2T_BEGIN(6);
+            // ---- last layer: 3 outputs (rows 0..2 of one tile), sigmoid, masked MSE, d rgb
+            float g[3] = {0.f, 0.f, 0.f};
+            {
+                const char* slot = stage_begin(false);
+                f32x16 acc = bias_init(ly_int(nl - 1, 2), 0);
+                gemm(acc, slot, Bh, Bl, NKH, MFt(), NKHt(), nohook, PcOn());
+                float* o = (a.rgb && valid && h == 0) ? a.rgb + ((size_t)b * Np + p) * 3 : dmy;
+                float yv[3] = {0.f, 0.f, 0.f};
+                if (h == 0) {
+                    const float m = valid ? (a.mask ? pro[3 * C::TPX + 32 * wave + pxl] : 1.0f) : 0.f;
+                    double sq = 0.0;
+                    float sqf = 0.f;
 #pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const float z = acc[c];
-                    const float yy = 1.0f / (1.0f + expf(-z));
-                    yv[c] = yy;
-                    const float t = valid ? pro[c * C::TPX + 32 * wave + pxl] : 0.f;
-                    // model/planar.py:388-390 and its autograd: x = (p - g) m, d = 2 x m
-                    const float xx = (yy - t) * m;
-                    sqf += xx * xx;
-                    const float d = (2.0f * xx) * m;
-                    g[c] = (d * (1.0f - yy)) * yy;  // sigmoid backward
+                    for (int c = 0; c < 3; ++c) {
+                        const float z = acc[c];
+                        const float yy = 1.0f / (1.0f + expf(-z));
+                        yv[c] = yy;
+                        const float t = valid ? pro[c * C::TPX + 32 * wave + pxl] : 0.f;
+                        // model/planar.py:388-390 and its autograd: x = (p - g) m, d = 2 x m
+                        const float xx = (yy - t) * m;
+                        sqf += xx * xx;
+                        const float d = (2.0f * xx) * m;
+                        g[c] = (d * (1.0f - yy)) * yy;  // sigmoid backward
+                    }
+                    sq = (double)sqf;
+                    lsq += sq;
+                    lms += (double)m;
+                    bl0 += g[0];
+                    bl1 += g[1];
+                    bl2 += g[2];
                 }
-                sq = (double)sqf;
-                lsq += sq;
-                lms += (double)m;
-                bl0 += g[0];
-                bl1 += g[1];
-                bl2 += g[2];
+                s2_st12(o, yv[0], yv[1], yv[2]);
+                st_cur += 1;
             }
-            dma_flush();
-            s2_st12(o, yv[0], yv[1], yv[2]);
-            dummies(ST1t());
-        }
-        if (a.fwd_only) {  // render: the program holds the forward stages only
+            if (a.fwd_only) {  // render: the program holds the forward stages only
+                S2T_END(6);
+                continue;
+            }
+            // g operand of the last-layer dgrad: lane half 0, k = [g hi (3), 0, g lo (3), 0]
+            S2Frag Bg;
+            {
+                float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                if (h == 0) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        f[c] = g[c];                                        // bf16(g) below
+                        f[4 + c] = g[c] - s2_lo16(s2_pk(g[c], 0.f));         // g - bf16(g)
+                    }
+                }
+                S2Frag dumm;
+                s2_split8<false>(f, Bg, dumm);
+            }
+            // ---- last-layer weight gradient of the wave's 32 pixels: dW[c][k] += sum_px g[c] feat[k]
+            //      16x16x32 MFMA: A = g^T (rows 0-2 hi, 4-6 lo; K = 32 pixels) from a wave-private
+            //      LDS image, B = feat^T per 16-feature k-step through a transposing LDS round trip
+            {
+                if (h == 0) {
+                    const uint32_t w0 = Bg.u.x, w1 = Bg.u.y, w2 = Bg.u.z, w3 = Bg.u.w;
+                    gts[0 * 32 + pxl] = (u16)(w0 & 0xffff);
+                    gts[1 * 32 + pxl] = (u16)(w0 >> 16);
+                    gts[2 * 32 + pxl] = (u16)(w1 & 0xffff);
+                    gts[4 * 32 + pxl] = (u16)(w2 & 0xffff);
+                    gts[5 * 32 + pxl] = (u16)(w2 >> 16);
+                    gts[6 * 32 + pxl] = (u16)(w3 & 0xffff);
+                }
+                const bf16x8 ga = *reinterpret_cast<const bf16x8*>(gts + (lane & 15) * 32 + 8 * (lane >> 4));
+                const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+                const int nkl = a.Kl / 16;
+#pragma unroll
+                for (int ks = 0; ks < NKH; ++ks) {
+                    if (ks < nkl) {
+                        *reinterpret_cast<uint4*>(trs + (pxl * 2 + h) * 8) = Bh[ks].u;
+                        const u16* b0 = trs + (8 * gq + q) * 16 + (pp & 1) * 8 + 4 * (pp >> 1);
+                        i16x4 vv[2] = {s2_tr16(b0), s2_tr16(b0 + 4 * 16)};
+                        const f32x4 r4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, *reinterpret_cast<bf16x8*>(vv), (f32x4){}, 0, 0, 0);
+                        float lo[3];
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) lo[c] = __shfl_down(r4[c], 16, 64);
+                        if (lane < 16) {
+#pragma unroll
+                            for (int c = 0; c < 3; ++c) wla[c * a.Kl + 16 * ks + lane] += r4[c] + lo[c];
+                        }
+                    }
+                }
+            }
+            {
+                SetSt cs;
+                cs.g = Bg;
+                cs.X0 = X[0];
+                cs.X1 = X[1];
+                cs.X2 = X[2];
+                cs.tile = tile;
+                if (si == 0) ss[0] = cs;
+                else ss[NS - 1] = cs;
+            }
             S2T_END(6);
-            continue;
         }
-        // g operand of the last-layer dgrad: lane half 0, k = [g hi (3), 0, g lo (3), 0]
-        S2Frag Bg;
-        {
-            float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            if (h == 0) {
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    f[c] = g[c];                                        // bf16(g) below
-                    f[4 + c] = g[c] - s2_lo16(s2_pk(g[c], 0.f));         // g - bf16(g)
-                }
-            }
-            S2Frag dumm;
-            s2_split8<false>(f, Bg, dumm);
-        }
-        // ---- last-layer weight gradient of the wave's 32 pixels: dW[c][k] += sum_px g[c] feat[k]
-        //      16x16x32 MFMA: A = g^T (rows 0-2 hi, 4-6 lo; K = 32 pixels) from a wave-private
-        //      LDS image, B = feat^T per 16-feature k-step through a transposing LDS round trip
-        {
-            if (h == 0) {
-                const uint32_t w0 = Bg.u.x, w1 = Bg.u.y, w2 = Bg.u.z, w3 = Bg.u.w;
-                gts[0 * 32 + pxl] = (u16)(w0 & 0xffff);
-                gts[1 * 32 + pxl] = (u16)(w0 >> 16);
-                gts[2 * 32 + pxl] = (u16)(w1 & 0xffff);
-                gts[4 * 32 + pxl] = (u16)(w2 & 0xffff);
-                gts[5 * 32 + pxl] = (u16)(w2 >> 16);
-                gts[6 * 32 + pxl] = (u16)(w3 & 0xffff);
-            }
-            const bf16x8 ga = *reinterpret_cast<const bf16x8*>(gts + (lane & 15) * 32 + 8 * (lane >> 4));
-            const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-            const int nkl = a.Kl / 16;
-#pragma unroll
-            for (int ks = 0; ks < NKH; ++ks) {
-                if (ks < nkl) {
-                    *reinterpret_cast<uint4*>(trs + (pxl * 2 + h) * 8) = Bh[ks].u;
-                    const u16* b0 = trs + (8 * gq + q) * 16 + (pp & 1) * 8 + 4 * (pp >> 1);
-                    i16x4 vv[2] = {s2_tr16(b0), s2_tr16(b0 + 4 * 16)};
-                    const f32x4 r4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, *reinterpret_cast<bf16x8*>(vv), (f32x4){}, 0, 0, 0);
-                    float lo[3];
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) lo[c] = __shfl_down(r4[c], 16, 64);
-                    if (lane < 16) {
-#pragma unroll
-                        for (int c = 0; c < 3; ++c) wla[c * a.Kl + 16 * ks + lane] += r4[c] + lo[c];
-                    }
-                }
-            }
+        if (a.fwd_only) continue;
+        if (nset < NS) {  // no tile for the last set: its dgrad runs on zeros into the store sink rows
+            SetSt cs;
+            cs.g.u = make_uint4(0, 0, 0, 0);
+            cs.X0 = cs.X1 = 0.f;
+            cs.X2 = 1.f;
+            cs.tile = -1;
+            ss[NS - 1] = cs;
         }
 
-        S2T_END(6);
         S2T_BEGIN(2);
+        // ---- the dgrad pass of the group's NS pixel sets: every weight stage is read once for all
+        //      of them, one GEMM pass per set.  Items i = NS rt + s in order; the epilogue of item
+        //      i-1 (mask, bf16 pack, stores) runs beside the MFMAs of item i, so one accumulator per
+        //      parity of i suffices.  Per set the MFMA sequence, epilogue and stores are those of a
+        //      single tile.
+        long long sl0[NS];  // the sets' first pixel slot of the wave (wave-uniform)
+        s2_sfor<NS>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            const int tl = ss[s].tile;
+            long long v;
+            if (tl < 0) {
+                v = a.S + 32 * wave;
+            } else {
+                const int bb = tl / tpp;
+                v = (long long)bb * a.geo.Np_pad + (tl - bb * tpp) * C::TPX + 32 * wave;
+            }
+            sl0[s] = v;
+        });
+        auto myslot_of = [&](int s) -> long long { return sl0[s] + pxl; };
+        // operand / output fragments of set s: the forward's arrays (the dgrad needs hi only, so the
+        // lo arrays carry the second set; reusing them keeps no extra array live across the pass)
+        S2Frag* const Dh[2] = {Bh, Bl};
+        S2Frag* const Do[2] = {Oh, Ol};
+        EpSt eb;
+        auto mks_b = [&](int s) -> const uint32_t* { return mkl + s * C::MSET; };
         // ---- last-layer dgrad: dfeat_{n-1} = W_{n-1}^T g, mask -> dz_{n-1}; one stage holds every
-        //      row tile's single k-step (tile rt at rt KB), epilogues pipelined across the tiles
+        //      row tile's single k-step (tile rt at rt KB)
         {
             const int lmask = nl - 2;
             const int nrt = ly_int(nl - 1, 1);
             u16* sbase = ly_ptr(nl - 1, 1);
             const int sld = ly_int(nl - 1, 4);
-            S2Frag gB[1] = {Bg};
-            const char* slot = stage_begin();
+            S2Frag gB[NS];
+            s2_sfor<NS>([&](auto sc) { gB[decltype(sc)::value] = ss[decltype(sc)::value].g; });
+            const char* slot = stage_begin(true);  // single-k-step GEMMs: the pieces in a burst
             s2_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;
-                f32x16& cur = (rt & 1) ? acc1 : acc0;
-                f32x16& prv = (rt & 1) ? acc0 : acc1;
                 if (rt < nrt) {
-                    cur = (f32x16){};
-                    if constexpr (rt == 0) {
-                        gemm(cur, slot, gB, gB, 1, MBt(), NK1t(), nohook);
-                    } else {
-                        ep.mw = mkl[(lmask * C::NMW + ((rt - 1) >> 1)) * 64 + lane];
-                        gemm(cur, slot + rt * 1024, gB, gB, 1, MBt(), NK1t(), [&](auto, auto pc) {
-                            s2_sfor<8>([&](auto ec) {
-                                bstep(prv, std::integral_constant<int, 8 * decltype(pc)::value + decltype(ec)::value>(),
-                                      std::integral_constant<int, rt - 1>());
-                            });
-                        });
-                        bfinish(std::integral_constant<int, rt - 1>(), sbase, sld);
-                    }
-                    if (rt == nrt - 1) {
-                        ep.mw = mkl[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
-                        s2_sfor<16>([&](auto ec) { bstep(cur, ec, rtc); });
-                        bfinish(rtc, sbase, sld);
-                    }
+                    s2_sfor<NS>([&](auto sc) {
+                        constexpr int s = decltype(sc)::value, i = rt * NS + s;
+                        constexpr int sp = (i + NS - 1) % NS, rp = (i - 1 + NS) / NS - 1;  // item i-1
+                        f32x16& cur = (i & 1) ? acc1 : acc0;
+                        f32x16& prv = (i & 1) ? acc0 : acc1;
+                        cur = (f32x16){};
+                        if constexpr (i == 0) {
+                            gemm(cur, slot, &gB[s], &gB[s], 1, MBt(), NK1t(), nohook, PcOff());
+                        } else {
+                            eb.mw = mks_b(sp)[(lmask * C::NMW + (rp >> 1)) * 64 + lane];
+                            gemm(cur, slot + rt * 1024, &gB[s], &gB[s], 1, MBt(), NK1t(), [&](auto, auto pc) {
+                                s2_sfor<8>([&](auto ec) {
+                                    bstep(eb, prv, std::integral_constant<int, 8 * decltype(pc)::value + decltype(ec)::value>(),
+                                          std::integral_constant<int, rp>());
+                                });
+                            }, PcOff());
+                            bfinish(eb, Do[sp], std::integral_constant<int, rp>(), sbase, sld, myslot_of(sp));
+                        }
+                        if (s == NS - 1 && rt == nrt - 1) {
+                            eb.mw = mks_b(s)[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
+                            s2_sfor<16>([&](auto ec) { bstep(eb, cur, ec, rtc); });
+                            bfinish(eb, Do[s], rtc, sbase, sld, myslot_of(s));
+                        }
+                    });
                 } else {
-                    zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
+                    s2_sfor<NS>([&](auto sc) {
+                        constexpr int s = decltype(sc)::value;
+                        Do[s][2 * rt].u = Do[s][2 * rt + 1].u = make_uint4(0, 0, 0, 0);
+                    });
                 }
             });
 #pragma unroll
-            for (int k = 0; k < NKH; ++k) Bh[k] = Oh[k];
+            for (int k = 0; k < NKH; ++k)
+                s2_sfor<NS>([&](auto sc) { Dh[decltype(sc)::value][k] = Do[decltype(sc)::value][k]; });
         }
         // ---- hidden dgrad chain l = nl-2 .. 1
         for (int l = nl - 2; l >= 1; --l) {
@@ -837,40 +940,53 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const int sld = ly_int(l, 4);
             s2_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;
-                f32x16& cur = (rt & 1) ? acc1 : acc0;
-                f32x16& prv = (rt & 1) ? acc0 : acc1;
                 if (rt < nrt) {
-                    const char* slot = stage_begin();
-                    cur = (f32x16){};
-                    if constexpr (rt == 0) {
-                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), nohook);
-                        dummies(STt());
-                    } else {
-                        ep.mw = mkl[(lmask * C::NMW + ((rt - 1) >> 1)) * 64 + lane];
-                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), [&](auto ksc, auto pc) {
-                            if constexpr (decltype(pc)::value == 0) bstep(prv, ksc, std::integral_constant<int, rt - 1>());
-                        });
-                        bfinish(std::integral_constant<int, rt - 1>(), sbase, sld);
-                    }
-                    if (rt == nrt - 1) {
-                        ep.mw = mkl[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
-                        s2_sfor<16>([&](auto ec) { bstep(cur, ec, rtc); });
-                        bfinish(rtc, sbase, sld);
-                    }
+                    const char* slot = stage_begin(false);
+                    s2_sfor<NS>([&](auto sc) {
+                        constexpr int s = decltype(sc)::value, i = rt * NS + s;
+                        constexpr int sp = (i + NS - 1) % NS, rp = (i - 1 + NS) / NS - 1;
+                        f32x16& cur = (i & 1) ? acc1 : acc0;
+                        f32x16& prv = (i & 1) ? acc0 : acc1;
+                        cur = (f32x16){};
+                        if constexpr (i == 0) {
+                            gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), nohook, std::integral_constant<bool, s == 0>());
+                        } else {
+                            eb.mw = mks_b(sp)[(lmask * C::NMW + (rp >> 1)) * 64 + lane];
+                            gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), [&](auto ksc, auto pc) {
+                                if constexpr (decltype(pc)::value == 0) bstep(eb, prv, ksc, std::integral_constant<int, rp>());
+                            }, std::integral_constant<bool, s == 0>());
+                            bfinish(eb, Do[sp], std::integral_constant<int, rp>(), sbase, sld, myslot_of(sp));
+                        }
+                        if (s == NS - 1 && rt == nrt - 1) {
+                            eb.mw = mks_b(s)[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
+                            s2_sfor<16>([&](auto ec) { bstep(eb, cur, ec, rtc); });
+                            bfinish(eb, Do[s], rtc, sbase, sld, myslot_of(s));
+                        }
+                    });
                 } else {
-                    zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
+                    s2_sfor<NS>([&](auto sc) {
+                        constexpr int s = decltype(sc)::value;
+                        Do[s][2 * rt].u = Do[s][2 * rt + 1].u = make_uint4(0, 0, 0, 0);
+                    });
                 }
             });
 #pragma unroll
-            for (int k = 0; k < NKH; ++k) Bh[k] = Oh[k];
+            for (int k = 0; k < NKH; ++k)
+                s2_sfor<NS>([&](auto sc) { Dh[decltype(sc)::value][k] = Do[decltype(sc)::value][k]; });
         }
         // ---- layer-0 dgrad + posenc adjoint: row (tile t, register r) = slot 16 t + r of the
         //      lane's coordinate: slot 2k = sin band k, 2k + 1 = cos band k, 2L = the raw coordinate.
-        //      The adjoint of tile t-1 (8 bands) runs beside the MFMAs of tile t.
-        float dc = 0.f;
+        //      The adjoint of item i-1 (8 bands) runs beside the MFMAs of item i.
+        float dc[NS], cds[NS];
+        s2_sfor<NS>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            dc[s] = 0.f;
+            const float dd = ss[s].X2 + 1e-8f;  // warp_point's (u, v), bit for bit
+            cds[s] = h ? ss[s].X1 / dd : ss[s].X0 / dd;
+        });
         {
             const int nta = a.nta;
-            auto adj_band = [&](const f32x16& pa, int t, auto ic) {
+            auto adj_band = [&](float& d, const float cd, const f32x16& pa, int t, auto ic) {
                 constexpr int i = decltype(ic)::value;
                 const int k = 8 * t + i;
                 if (k < L) {
@@ -882,37 +998,39 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         gs = gs * w;
                         gc = gc * w;
                     }
-                    dc += (gs * co - gc * sn) * ldexpf(pi_f, k);
+                    d += (gs * co - gc * sn) * ldexpf(pi_f, k);
                 }
             };
-            auto adj_raw = [&](const f32x16& pa, int t) {
+            auto adj_raw = [&](float& d, const f32x16& pa, int t) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
-                    if (16 * t + r == 2 * L) dc += pa[r];
+                    if (16 * t + r == 2 * L) d += pa[r];
             };
             s2_sfor<C::NTA>([&](auto tc) {
                 constexpr int t = decltype(tc)::value;
-                f32x16& cur = (t & 1) ? acc1 : acc0;
-                f32x16& prv = (t & 1) ? acc0 : acc1;
                 if (t < nta) {
-                    const char* slot = stage_begin();
-                    cur = (f32x16){};
-                    if constexpr (t == 0) {
-                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), nohook);
-                    } else {
-                        gemm(cur, slot, Bh, Bh, NKH, MBt(), NKHt(), [&](auto ksc, auto pc) {
-                            constexpr int ks = decltype(ksc)::value;
-                            if constexpr ((ks & 1) == 0 && decltype(pc)::value == 0)
-                                adj_band(prv, t - 1, std::integral_constant<int, ks / 2>());
-                        });
-                        adj_raw(prv, t - 1);
-                    }
-                    if (t == nta - 1) {
-                        s2_sfor<8>([&](auto ic) { adj_band(cur, t, ic); });
-                        adj_raw(cur, t);
-                    } else {
-                        dummies(STt());
-                    }
+                    const char* slot = stage_begin(false);
+                    s2_sfor<NS>([&](auto sc) {
+                        constexpr int s = decltype(sc)::value, i = t * NS + s;
+                        constexpr int sp = (i + NS - 1) % NS, tp = (i - 1 + NS) / NS - 1;
+                        f32x16& cur = (i & 1) ? acc1 : acc0;
+                        f32x16& prv = (i & 1) ? acc0 : acc1;
+                        cur = (f32x16){};
+                        if constexpr (i == 0) {
+                            gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), nohook, std::integral_constant<bool, s == 0>());
+                        } else {
+                            gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), [&](auto ksc, auto pc) {
+                                constexpr int ks = decltype(ksc)::value;
+                                if constexpr ((ks & 1) == 0 && decltype(pc)::value == 0)
+                                    adj_band(dc[sp], cds[sp], prv, tp, std::integral_constant<int, ks / 2>());
+                            }, std::integral_constant<bool, s == 0>());
+                            adj_raw(dc[sp], prv, tp);
+                        }
+                        if (s == NS - 1 && t == nta - 1) {
+                            s2_sfor<8>([&](auto ic) { adj_band(dc[s], cds[s], cur, t, ic); });
+                            adj_raw(dc[s], cur, t);
+                        }
+                    });
                 }
             });
         }
@@ -920,35 +1038,51 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         S2T_BEGIN(3);
         // (u, v) = X[:2] / (X[2] + 1e-8) backward, then the bmm backward -> dH partial of the wave
         {
-            const float dother = __shfl_xor(dc, 32, 64);
-            const float du = h ? dother : dc, dv = h ? dc : dother;
-            float h9[9];
-#pragma unroll
-            for (int e = 0; e < 9; ++e) h9[e] = 0.f;
-            if (h == 0 && valid) {
-                const float dd = X[2] + 1e-8f;
-                const float dX0 = du / dd, dX1 = dv / dd;
-                const float dd2 = dd * dd;
-                const float dX2 = (-du * X[0]) / dd2 + (-dv * X[1]) / dd2;
-                const float hom[3] = {x, y, 1.f};
-#pragma unroll
-                for (int cc = 0; cc < 3; ++cc) {
-                    h9[0 + cc] = dX0 * hom[cc];
-                    h9[3 + cc] = dX1 * hom[cc];
-                    h9[6 + cc] = dX2 * hom[cc];
+            float mine[NS];
+            float* dst[NS];
+            s2_sfor<NS>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                const SetSt& cs = ss[s];
+                const float dother = __shfl_xor(dc[s], 32, 64);
+                const float du = h ? dother : dc[s], dv = h ? dc[s] : dother;
+                // the set's grid point (as the prologue computed it) and validity
+                bool valid = false;
+                float x = 0.f, y = 0.f;
+                if (cs.tile >= 0) {
+                    const int bb = cs.tile / tpp;
+                    const int p = (cs.tile - bb * tpp) * C::TPX + 32 * wave + pxl;
+                    valid = p < Np;
+                    const int r = p / a.geo.w, cc = p - r * a.geo.w;
+                    x = grid_coord(a.geo.x0 + cc, a.geo.W, a.geo.norm_w);
+                    y = grid_coord(a.geo.y0 + r, a.geo.H, a.geo.norm_h);
                 }
-            }
-            float mine = 0.f;
+                float h9[9];
 #pragma unroll
-            for (int e = 0; e < 9; ++e) {
-                const float s = wave_total63(h9[e]);
-                const float sb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 63));
-                if (lane == e) mine = sb;
-            }
-            float* dst = lane < 9 ? a.dH_partial + (size_t)(slot0 / 32) * 9 + lane : dmy;
-            dma_flush();
-            s2_st4(dst, mine);
-            dummies(ST1t());
+                for (int e = 0; e < 9; ++e) h9[e] = 0.f;
+                if (h == 0 && valid) {
+                    const float dd = cs.X2 + 1e-8f;
+                    const float dX0 = du / dd, dX1 = dv / dd;
+                    const float dd2 = dd * dd;
+                    const float dX2 = (-du * cs.X0) / dd2 + (-dv * cs.X1) / dd2;
+                    const float hom[3] = {x, y, 1.f};
+#pragma unroll
+                    for (int cc = 0; cc < 3; ++cc) {
+                        h9[0 + cc] = dX0 * hom[cc];
+                        h9[3 + cc] = dX1 * hom[cc];
+                        h9[6 + cc] = dX2 * hom[cc];
+                    }
+                }
+                mine[s] = 0.f;
+#pragma unroll
+                for (int e = 0; e < 9; ++e) {
+                    const float sm = wave_total63(h9[e]);
+                    const float sb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm), 63));
+                    if (lane == e) mine[s] = sb;
+                }
+                dst[s] = lane < 9 ? a.dH_partial + (size_t)(sl0[s] / 32) * 9 + lane : dmy;
+            });
+            s2_sfor<NS>([&](auto sc) { s2_st4(dst[decltype(sc)::value], mine[decltype(sc)::value]); });
+            st_cur += NS;
         }
         S2T_END(3);
     }
@@ -987,7 +1121,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     for (int e = threadIdx.x; e < 3 * a.Kl; e += NW * 64) {
         float s = 0.f;
         for (int w = 0; w < NW; ++w)
-            s += reinterpret_cast<const float*>(smem + a.lds_wave + w * a.lds_wave_bytes + 2048 + MAXR * C::NMW * 256)[e];
+            s += reinterpret_cast<const float*>(smem + a.lds_wave + w * a.lds_wave_bytes + 2048 + NS * C::MSET * 4)[e];
         a.wlast_partial[(size_t)blockIdx.x * 3 * a.Kl + e] = s;
     }
 }

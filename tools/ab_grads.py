@@ -1,5 +1,6 @@
-"""Dump the gradients of one fused bf16 training step at C3 widths (8 patches) so two library
-builds can be compared bit for bit:  MARF_LIB=<lib> python tools/ab_grads.py out.npz
+"""Dump the gradients of two fused training steps at C3 widths so two library builds can be
+compared bit for bit:  MARF_LIB=<lib> python tools/ab_grads.py out.npz [precision] [patches]
+(default bf16, 8 patches; 4 or 12 patches give the step kernel an odd tile count per block)
 then  python tools/ab_grads.py --compare a.npz b.npz"""
 import os
 import sys
@@ -9,7 +10,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def dump(path):
+def dump(path, precision="bf16", B=8):
     import torch
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "masking-bundle-adjusting-neural-radiance-fields_amd"))
@@ -17,8 +18,7 @@ def dump(path):
     from model import planar
     from util import EasyDict as edict
     dev = torch.device("cuda", 0)
-    B = 8
-    opt = bench.make_opt("c3", "bf16", B)
+    opt = bench.make_opt("c3", precision, B)
     opt.device = str(dev)
     torch.manual_seed(3)
     graph = planar.Graph(opt).to(dev)
@@ -59,4 +59,4 @@ def compare(a, b):
 if __name__ == "__main__":
     if sys.argv[1] == "--compare":
         sys.exit(1 if compare(sys.argv[2], sys.argv[3]) else 0)
-    dump(sys.argv[1])
+    dump(sys.argv[1], *(sys.argv[2:3] or ["bf16"]), *[int(x) for x in sys.argv[3:4]])
