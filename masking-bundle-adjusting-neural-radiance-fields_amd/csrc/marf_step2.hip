@@ -60,6 +60,14 @@ MARF_DEV void s2_st16(void* dst, uint4 u) {
     const s2_u32x4 v = {u.x, u.y, u.z, u.w};
     asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
+template <int OFF>
+MARF_DEV void s2_st16o(void* base, uint4 u) {  // 16 B at base + OFF bytes (instruction offset)
+#ifdef S2_DIAG_NOSTORE
+    return;
+#endif
+    const s2_u32x4 v = {u.x, u.y, u.z, u.w};
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2\n\ts_nop 1" ::"v"(base), "v"(v), "n"(OFF) : "memory");
+}
 MARF_DEV void s2_st12(void* dst, float a, float b, float c) {
     typedef float f32x3 __attribute__((ext_vector_type(3)));
     f32x3 v = {a, b, c};
@@ -336,15 +344,17 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     //  pixel holds columns 16 ks + 4 h + 0..3 (dwords x, y) and 16 ks + 8 + 4 h + 0..3 (z, w); two
     //  v_permlane32_swap exchange the lane halves' x, y <-> z, w so that lane (p, h) holds columns
     //  16 ks + 8 h + 0..7 contiguously: one 16-B store per lane per k-step, 2 per row tile)
-    auto store_rt = [&](u16* base, int ld, long long slot, int rt, const S2Frag& f0, const S2Frag& f1) {
-        u16* row = base + slot * ld + 32 * rt + 8 * h;
+    //  row0 = the lane's row base (tensor + slot * ld + 8 h), the row tile's column offset is the
+    //  stores' instruction offset)
+    auto store_rt = [&](u16* row0, auto rtc, const S2Frag& f0, const S2Frag& f1) {
+        constexpr int rt = decltype(rtc)::value;
         auto contig = [&](const S2Frag& f) -> uint4 {
             const auto xz = __builtin_amdgcn_permlane32_swap(f.u.x, f.u.z, false, false);
             const auto yw = __builtin_amdgcn_permlane32_swap(f.u.y, f.u.w, false, false);
             return make_uint4(xz[0], yw[0], xz[1], yw[1]);
         };
-        s2_st16(row, contig(f0));
-        s2_st16(row + 16, contig(f1));
+        s2_st16o<64 * rt>(row0, contig(f0));
+        s2_st16o<64 * rt + 32>(row0, contig(f1));
         st_cur += 2;
     };
 
@@ -481,7 +491,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         o0.u = o1.u = q0.u = q1.u = make_uint4(0, 0, 0, 0);
     };
     // pipelined epilogues: micro-steps of one 32-row accumulator tile
-    long long myslot_g = 0;
     struct EpSt {
         uint32_t bits, mw;
         float vp, xo;
@@ -542,7 +551,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         fpack(ec);
     };
     // forward finish of tile rt: operand fragments of k-steps 2 rt, 2 rt + 1, mask word, 2 stores
-    auto ffinish = [&](int l, auto rtc, bool save, u16* sbase, int sld, uint32_t* mks) {
+    auto ffinish = [&](int l, auto rtc, bool save, u16* srow, uint32_t* mks) {
         constexpr int rt = decltype(rtc)::value;
 #ifdef S2_DIAG_NOEPI
         return;
@@ -555,7 +564,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         }
         if constexpr ((rt & 1) == 0) mpend = ep.bits << 16;
         else mks[(l * C::NMW + (rt >> 1)) * 64 + lane] = mpend | ep.bits;
-        if (save) store_rt(sbase, sld, myslot_g, rt, Oh[2 * rt], Oh[2 * rt + 1]);
+        if (save) store_rt(srow, rtc, Oh[2 * rt], Oh[2 * rt + 1]);
     };
     // dgrad step e: dz = acc * relu'(z) with the mask word e.mw
     auto bstep = [&](EpSt& es, const f32x16& pa, auto ec, auto rtc) {
@@ -579,14 +588,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             es.vp = x;
         }
     };
-    auto bfinish = [&](EpSt& es, S2Frag* O, auto rtc, u16* sbase, int sld, long long slot) {
+    auto bfinish = [&](EpSt& es, S2Frag* O, auto rtc, u16* row0) {
         constexpr int rt = decltype(rtc)::value;
 #ifdef S2_DIAG_NOEPI
         return;
 #endif
         O[2 * rt].u = make_uint4(es.hw[0], es.hw[1], es.hw[2], es.hw[3]);
         O[2 * rt + 1].u = make_uint4(es.hw[4], es.hw[5], es.hw[6], es.hw[7]);
-        store_rt(sbase, sld, slot, rt, O[2 * rt], O[2 * rt + 1]);
+        store_rt(row0, rtc, O[2 * rt], O[2 * rt + 1]);
     };
     const float pi_f = 3.14159265358979323846f;
 
@@ -611,7 +620,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const int p0 = (tile - b * tpp) * C::TPX + 32 * wave;
             const long long slot0 = (long long)b * a.geo.Np_pad + p0;
             const long long myslot = slot0 + pxl;
-            myslot_g = myslot;
             const int p = p0 + pxl;
             const bool valid = p < Np;
             const float* pro = pro_buf(pb);
@@ -696,8 +704,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 typedef std::integral_constant<bool, decltype(nk_tag)::value == NKH> PcL;  // hidden: pieces in the GEMM
                 const int nrt = ly_int(l, 0);
                 const bool save = l + 1 < nl - 1 && !a.fwd_only;
-                u16* sbase = save ? ly_ptr(l + 1, 0) : nullptr;
-                const int sld = save ? ly_int(l + 1, 3) : 0;
+                u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) + 8 * h : nullptr;
                 const int boff = ly_int(l, 2);
                 const char* slot0 = nullptr;
                 s2_sfor<NRT>([&](auto rtc) {
@@ -707,12 +714,13 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                     if (rt < nrt) {
                         // layer 0: r0 row tiles share a stage (their few k-steps fill one slot)
                         const int sub = l == 0 ? rt % a.r0 : 0;
+                        // the bias (a static LDS table) before the stage wait: its reads overlap it
+                        cur = bias_init(boff, rt);
                         if (sub == 0) slot0 = stage_begin(l == 0);  // layer 0: the pieces in a burst
                         const char* slot = slot0 + sub * a.nk0 * 1024;
                         // the next tile's target / mask / H into the other input buffer (the tile that
                         // read it last finished before this stage's barrier)
                         if (l == 0 && rt == 0 && ti + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
-                        cur = bias_init(boff, rt);
                         if constexpr (rt == 0) {
                             gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, nohook, PcL());
                         } else {
@@ -729,12 +737,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                             s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
                                 if (decltype(ec)::value >= MS * nk) fstep(prv, ec);
                             });
-                            ffinish(l, std::integral_constant<int, rt - 1>(), save, sbase, sld, mks);
+                            ffinish(l, std::integral_constant<int, rt - 1>(), save, srow, mks);
                         }
                         if (rt == nrt - 1) {
                             ep.bits = 0;
                             s2_sfor<16>([&](auto ec) { fstep(cur, ec); });
-                            ffinish(l, rtc, save, sbase, sld, mks);
+                            ffinish(l, rtc, save, srow, mks);
                         }
                     } else {
                         zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
@@ -754,8 +762,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             // ---- last layer: 3 outputs (rows 0..2 of one tile), sigmoid, masked MSE, d rgb
             float g[3] = {0.f, 0.f, 0.f};
             {
-                const char* slot = stage_begin(false);
                 f32x16 acc = bias_init(ly_int(nl - 1, 2), 0);
+                const char* slot = stage_begin(false);
                 gemm(acc, slot, Bh, Bl, NKH, MFt(), NKHt(), nohook, PcOn());
                 float* o = (a.rgb && valid && h == 0) ? a.rgb + ((size_t)b * Np + p) * 3 : dmy;
                 float yv[3] = {0.f, 0.f, 0.f};
@@ -889,8 +897,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         {
             const int lmask = nl - 2;
             const int nrt = ly_int(nl - 1, 1);
-            u16* sbase = ly_ptr(nl - 1, 1);
-            const int sld = ly_int(nl - 1, 4);
+            u16* brow[NS];
+            s2_sfor<NS>([&](auto sc) {
+                brow[decltype(sc)::value] = ly_ptr(nl - 1, 1) + myslot_of(decltype(sc)::value) * ly_int(nl - 1, 4) + 8 * h;
+            });
             S2Frag gB[NS];
             s2_sfor<NS>([&](auto sc) { gB[decltype(sc)::value] = ss[decltype(sc)::value].g; });
             const char* slot = stage_begin(true);  // single-k-step GEMMs: the pieces in a burst
@@ -913,12 +923,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                                           std::integral_constant<int, rp>());
                                 });
                             }, PcOff());
-                            bfinish(eb, Do[sp], std::integral_constant<int, rp>(), sbase, sld, myslot_of(sp));
+                            bfinish(eb, Do[sp], std::integral_constant<int, rp>(), brow[sp]);
                         }
                         if (s == NS - 1 && rt == nrt - 1) {
                             eb.mw = mks_b(s)[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
                             s2_sfor<16>([&](auto ec) { bstep(eb, cur, ec, rtc); });
-                            bfinish(eb, Do[s], rtc, sbase, sld, myslot_of(s));
+                            bfinish(eb, Do[s], rtc, brow[s]);
                         }
                     });
                 } else {
@@ -936,8 +946,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         for (int l = nl - 2; l >= 1; --l) {
             const int lmask = l - 1;
             const int nrt = ly_int(l, 1);
-            u16* sbase = ly_ptr(l, 1);
-            const int sld = ly_int(l, 4);
+            u16* brow[NS];
+            s2_sfor<NS>([&](auto sc) {
+                brow[decltype(sc)::value] = ly_ptr(l, 1) + myslot_of(decltype(sc)::value) * ly_int(l, 4) + 8 * h;
+            });
             s2_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;
                 if (rt < nrt) {
@@ -955,12 +967,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                             gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), [&](auto ksc, auto pc) {
                                 if constexpr (decltype(pc)::value == 0) bstep(eb, prv, ksc, std::integral_constant<int, rp>());
                             }, std::integral_constant<bool, s == 0>());
-                            bfinish(eb, Do[sp], std::integral_constant<int, rp>(), sbase, sld, myslot_of(sp));
+                            bfinish(eb, Do[sp], std::integral_constant<int, rp>(), brow[sp]);
                         }
                         if (s == NS - 1 && rt == nrt - 1) {
                             eb.mw = mks_b(s)[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
                             s2_sfor<16>([&](auto ec) { bstep(eb, cur, ec, rtc); });
-                            bfinish(eb, Do[s], rtc, sbase, sld, myslot_of(s));
+                            bfinish(eb, Do[s], rtc, brow[s]);
                         }
                     });
                 } else {
