@@ -191,7 +191,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     float* wla = reinterpret_cast<float*>(wpriv + 2048 + NS * C::MSET * 4);  // [3][Kl] dW_last
     float* dmy = a.dummy + (((size_t)blockIdx.x * NW + wave) * 2 * 64 + lane) * 2;
 #ifdef MARF_STAMPS
-    unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tacc[16] = {};
 #endif
 
     // ---- constants into LDS (plain loads: the compiler's waits are harmless before the ring)
@@ -722,9 +722,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         // read it last finished before this stage's barrier)
                         if (l == 0 && rt == 0 && ti + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
                         if constexpr (rt == 0) {
+                            S2T_BEGIN(8);
                             gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, nohook, PcL());
+                            S2T_END(8);
                         } else {
                             ep.bits = 0;
+                            S2T_BEGIN(8);
                             gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, [&](auto ksc, auto pc) {
                                 s2_sfor<MS>([&](auto jc) {
                                     constexpr int e = decltype(ksc)::value * MS + decltype(jc)::value;
@@ -734,6 +737,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                                     }
                                 });
                             }, PcL());
+                            S2T_END(8);
                             s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
                                 if (decltype(ec)::value >= MS * nk) fstep(prv, ec);
                             });
@@ -961,12 +965,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         f32x16& prv = (i & 1) ? acc0 : acc1;
                         cur = (f32x16){};
                         if constexpr (i == 0) {
+                            S2T_BEGIN(9);
                             gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), nohook, std::integral_constant<bool, s == 0>());
+                            S2T_END(9);
                         } else {
                             eb.mw = mks_b(sp)[(lmask * C::NMW + (rp >> 1)) * 64 + lane];
+                            S2T_BEGIN(9);
                             gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), [&](auto ksc, auto pc) {
                                 if constexpr (decltype(pc)::value == 0) bstep(eb, prv, ksc, std::integral_constant<int, rp>());
                             }, std::integral_constant<bool, s == 0>());
+                            S2T_END(9);
                             bfinish(eb, Do[sp], std::integral_constant<int, rp>(), brow[sp]);
                         }
                         if (s == NS - 1 && rt == nrt - 1) {
@@ -1029,13 +1037,17 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         f32x16& prv = (i & 1) ? acc0 : acc1;
                         cur = (f32x16){};
                         if constexpr (i == 0) {
+                            S2T_BEGIN(9);
                             gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), nohook, std::integral_constant<bool, s == 0>());
+                            S2T_END(9);
                         } else {
+                            S2T_BEGIN(9);
                             gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), [&](auto ksc, auto pc) {
                                 constexpr int ks = decltype(ksc)::value;
                                 if constexpr ((ks & 1) == 0 && decltype(pc)::value == 0)
                                     adj_band(dc[sp], cds[sp], prv, tp, std::integral_constant<int, ks / 2>());
                             }, std::integral_constant<bool, s == 0>());
+                            S2T_END(9);
                             adj_raw(dc[sp], prv, tp);
                         }
                         if (s == NS - 1 && t == nta - 1) {
@@ -1101,7 +1113,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     S2T_END(7);
 #ifdef MARF_STAMPS
     if (a.stamps && threadIdx.x == 0)
-        for (int k = 0; k < 8; ++k) a.stamps[(size_t)blockIdx.x * 8 + k] = tacc[k];
+        for (int k = 0; k < 16; ++k) a.stamps[(size_t)blockIdx.x * 16 + k] = tacc[k];
 #endif
 
     // ---- per-block partials (fixed order over waves)

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "masking-bundle-adjusting-neural-radiance-
 import bench  # noqa: E402
 
 NAMES = ["stage wait+barrier", "DMA issue", "backward (BWL..BW0)", "dH tail", "prologue", "forward (FW0..FWH)",
-         "last layer + dW_last", "tile loop total"]
+         "last layer + dW_last", "tile loop total", "  in fwd GEMM bodies", "  in dgrad GEMM bodies"]
 
 
 def main():
@@ -37,13 +37,13 @@ def main():
     m.graph.neural_image.progress.data.fill_(0.2)
     m.graph.need_edges = False
     var = edict(images=m.images)
-    stamps = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
     marf_hip.lib().marf_debug_set_stamps(marf_hip._ptr(stamps))
     for _ in range(3):
         v = m.graph.forward(var)
         m.graph.compute_loss(v).rgb.backward()
     torch.cuda.synchronize()
-    st = stamps.view(-1, 8).cpu().numpy().astype(np.float64)
+    st = stamps.view(-1, 16).cpu().numpy().astype(np.float64)[:, :10]
     st = st[st[:, 7] > 0]
     tiles = 4194304 // (32 * (4 if args.precision == "bf16x3" else 8)) / len(st)
     mean = st.mean(0) / tiles
