@@ -15,6 +15,6 @@ timeout -k 10 400 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err 
 tail -1 $OUT/bench_$TAG.json | cut -c1-600
 export TMPDIR=/tmp
 ROOT=$PWD
-cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_$TAG.log 2>&1
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render > $OUT/prof_$TAG.log 2>&1
 echo "rocprof exit $?"
 find $OUT/prof_$TAG -name "*stats*" | head
