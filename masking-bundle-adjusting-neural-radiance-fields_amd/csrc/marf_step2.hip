@@ -741,7 +741,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                             s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
                                 if (decltype(ec)::value >= MS * nk) fstep(prv, ec);
                             });
+                            S2T_BEGIN(10);
                             ffinish(l, std::integral_constant<int, rt - 1>(), save, srow, mks);
+                            S2T_END(10);
                         }
                         if (rt == nrt - 1) {
                             ep.bits = 0;
@@ -927,7 +929,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                                           std::integral_constant<int, rp>());
                                 });
                             }, PcOff());
+                            S2T_BEGIN(11);
                             bfinish(eb, Do[sp], std::integral_constant<int, rp>(), brow[sp]);
+                            S2T_END(11);
                         }
                         if (s == NS - 1 && rt == nrt - 1) {
                             eb.mw = mks_b(s)[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
@@ -975,7 +979,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                                 if constexpr (decltype(pc)::value == 0) bstep(eb, prv, ksc, std::integral_constant<int, rp>());
                             }, std::integral_constant<bool, s == 0>());
                             S2T_END(9);
+                            S2T_BEGIN(11);
                             bfinish(eb, Do[sp], std::integral_constant<int, rp>(), brow[sp]);
+                            S2T_END(11);
                         }
                         if (s == NS - 1 && rt == nrt - 1) {
                             eb.mw = mks_b(s)[(lmask * C::NMW + (rt >> 1)) * 64 + lane];

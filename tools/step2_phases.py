@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.join(ROOT, "masking-bundle-adjusting-neural-radiance-
 import bench  # noqa: E402
 
 NAMES = ["stage wait+barrier", "DMA issue", "backward (BWL..BW0)", "dH tail", "prologue", "forward (FW0..FWH)",
-         "last layer + dW_last", "tile loop total", "  in fwd GEMM bodies", "  in dgrad GEMM bodies"]
+         "last layer + dW_last", "tile loop total", "  in fwd GEMM bodies", "  in dgrad GEMM bodies",
+         "  fwd tile finish (frag regs, mask, stores)", "  dgrad tile finish (frag regs, stores)"]
 
 
 def main():
@@ -43,7 +44,7 @@ def main():
         v = m.graph.forward(var)
         m.graph.compute_loss(v).rgb.backward()
     torch.cuda.synchronize()
-    st = stamps.view(-1, 16).cpu().numpy().astype(np.float64)[:, :10]
+    st = stamps.view(-1, 16).cpu().numpy().astype(np.float64)[:, :12]
     st = st[st[:, 7] > 0]
     tiles = 4194304 // (32 * (4 if args.precision == "bf16x3" else 8)) / len(st)
     mean = st.mean(0) / tiles
