@@ -528,6 +528,54 @@ def test_fused_step_c3_linearity_and_determinism(tmp_path):
         assert torch.equal(a, b), (i, (a - b).abs().max().item())
 
 
+@pytest.mark.parametrize("grid", [255, 7, 1])
+def test_step2_tile_grouping_invariance(grid, tmp_path):
+    """The bf16x3 step kernel runs each block's tiles in pairs whose dgrad shares every weight stage
+    (marf_step2.hip); a block with an odd tile count ends on a single tile.  The per-pixel results
+    do not depend on how tiles are grouped: with 255, 7 and 1 blocks (odd and even tile counts per
+    block) instead of one block per CU, rgb, the hidden- and first-layer weight gradients (from the
+    saved tensors) and the warp gradient are bit-identical; the last layer's gradients and the
+    loss are block-partial sums, so they agree to summation order."""
+    from model import planar
+    from util import EasyDict as edict
+    B = 3
+    opt = make_opt(tmp_path, H=512, W=512, patch_H=256, patch_W=256, batch_size=B, precision="bf16x3",
+                   arch={"layers": [None, 256, 256, 256, 256, 3], "skip": [], "posenc": {"L_2D": 16}})
+    torch.manual_seed(0)
+    graph = planar.Graph(opt).to(DEV)
+    graph.neural_image.progress.data.fill_(0.2)
+    rng = np.random.default_rng(5)
+    gt = t(rng.random((B, 3, 256, 256)).astype(np.float32))
+    mask = t((rng.random((B, 1, 256, 256)) < 0.85).astype(np.float32))
+    var = edict(images=edict(rgb=gt, masks=mask, masks_eroded=mask, edges=None))
+    graph.need_edges = False
+    with torch.no_grad():
+        graph.warp_param.weight.copy_(t((rng.standard_normal((B, 8)) * 0.01).astype(np.float32)))
+
+    def run():
+        for q in graph.parameters():
+            q.grad = None
+        v = graph.forward(var)
+        loss = graph.compute_loss(v).rgb
+        loss.backward()
+        return (float(loss.detach()), v.rgb_prediction.detach().clone(),
+                [q.grad.clone() for q in graph.neural_image.mlp.parameters()], graph.warp_param.weight.grad.clone())
+
+    l0, rgb0, g0, w0 = run()
+    os.environ["MARF_STEP2_GRID"] = str(grid)
+    try:
+        l1, rgb1, g1, w1 = run()
+    finally:
+        del os.environ["MARF_STEP2_GRID"]
+    assert torch.equal(rgb0, rgb1)
+    assert torch.equal(w0, w1)
+    for i, (a, b) in enumerate(zip(g0[:-2], g1[:-2])):  # every layer but the last: bit-identical
+        assert torch.equal(a, b), (i, (a - b).abs().max().item())
+    for a, b in zip(g0[-2:], g1[-2:]):  # last layer: block partials in another order
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-7 * float(a.abs().max())), (a - b).abs().max().item()
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+
+
 def test_wgrad_dma_wide_layers_bitwise(tmp_path):
     """512-wide hidden layers (C5 shape): the LDS-DMA weight-gradient kernel splits each output in
     256 x 256 blocks (and layer 0 in 256 x 96 blocks); its gradients equal the register-staged
