@@ -68,6 +68,12 @@ int marf_version(void);
  * lie_batch: the batch size torch would see (selects torch's path; pass B unless sharded). */
 int marf_sl3_to_SL3(const float* d_h, float* d_H, int B, int lie_batch, void* stream);
 int marf_sl3_to_SL3_backward(const float* d_h, const float* d_dH, float* d_dh, int B, int lie_batch, void* stream);
+/* SE(2) warps (north_star "sl(3)/SE(2)"; an extension: the reference has sl(3) only, warp.py:72-80).
+ * se(2) tangent p = (tx, ty, theta) [B][3] -> the sl(3) parameters h [B][8] of the same generator
+ * [[0,-theta,tx],[theta,0,ty],[0,0,0]] in warp.py:101-104's layout; marf_sl3_to_SL3(h) is then the
+ * SE(2) exponential and every warp / step entry point takes h unchanged.  Backward: dp = adjoint(dh). */
+int marf_se2_to_sl3(const float* d_p, float* d_h, int B, void* stream);
+int marf_se2_to_sl3_backward(const float* d_dh, float* d_dp, int B, void* stream);
 
 /* ---- Warp (warp.py:33-68 get_normalized_pixel_grid, one copy [n][2]; warp.py:70-81 warp_grid) */
 int marf_pixel_grid(int H, int W, int patch_H, int patch_W, int crop, float* d_xy, void* stream);

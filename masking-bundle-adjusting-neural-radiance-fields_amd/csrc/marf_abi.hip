@@ -141,6 +141,18 @@ int marf_sl3_to_SL3_backward(const float* d_h, const float* d_dH, float* d_dh, i
     return MARF_OK;
 }
 
+int marf_se2_to_sl3(const float* d_p, float* d_h, int B, void* stream) {
+    if (B < 0 || (B > 0 && (!d_p || !d_h))) return fail(MARF_ERR_INVALID, "se2_to_sl3: bad arguments");
+    HIPCHK(marf_launch_se2_embed(d_p, d_h, B, (hipStream_t)stream), "se2_to_sl3");
+    return MARF_OK;
+}
+
+int marf_se2_to_sl3_backward(const float* d_dh, float* d_dp, int B, void* stream) {
+    if (B < 0 || (B > 0 && (!d_dh || !d_dp))) return fail(MARF_ERR_INVALID, "se2_to_sl3_backward: bad arguments");
+    HIPCHK(marf_launch_se2_embed_bwd(d_dh, d_dp, B, (hipStream_t)stream), "se2_to_sl3_backward");
+    return MARF_OK;
+}
+
 static int make_geo(const marf_geometry* g, GeoDev& d, int TP_pad) {
     if (!g) return fail(MARF_ERR_INVALID, "geometry is NULL");
     memset(&d, 0, sizeof(d));

@@ -131,6 +131,8 @@ hipError_t ensure_dynamic_lds(const void* kernel, size_t lds);
 }  // namespace marf
 
 hipError_t marf_launch_sl3(const float* h, float* H, int B, int batch_hint, hipStream_t s);
+hipError_t marf_launch_se2_embed(const float* p, float* h, int B, hipStream_t s);
+hipError_t marf_launch_se2_embed_bwd(const float* dh, float* dp, int B, hipStream_t s);
 hipError_t marf_launch_sl3_bwd(const float* h, const float* dH, float* dh, int B, int batch_hint, hipStream_t s);
 hipError_t marf_launch_reduce_dH(const float* partial, int tiles_per_patch, int B, const float* h, float* dH_out,
                                  float* dh, int batch_hint, hipStream_t s, const float* gscale = nullptr,

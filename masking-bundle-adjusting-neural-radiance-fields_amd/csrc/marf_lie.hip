@@ -309,9 +309,50 @@ __global__ void k_reduce_dH_lie_bwd(const float* __restrict__ partial, int tiles
     }
 }
 
+// SE(2) as a sub-algebra of the reference's sl(3) parametrisation (an extension: the reference
+// warps with sl(3) only, warp.py:72-80).  se(2) tangent p = (tx, ty, theta) -> the generator
+// [[0, -theta, tx], [theta, 0, ty], [0, 0, 0]], which in warp.py:101-104's layout
+// A = [[h5, h3, h1], [h4, -h5-h6, h2], [h7, h8, h6]] is h = (tx, ty, -theta, theta, 0, 0, 0, 0);
+// marf_sl3_to_SL3 of that h is the SE(2) exponential.  Backward: the adjoint of the embedding.
+__global__ void k_se2_to_sl3(const float* __restrict__ p, float* __restrict__ h, int B) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const float tx = p[3 * b], ty = p[3 * b + 1], th = p[3 * b + 2];
+    float* o = h + 8 * (size_t)b;
+    o[0] = tx;
+    o[1] = ty;
+    o[2] = -th;
+    o[3] = th;
+    o[4] = 0.f;
+    o[5] = 0.f;
+    o[6] = 0.f;
+    o[7] = 0.f;
+}
+
+__global__ void k_se2_to_sl3_bwd(const float* __restrict__ dh, float* __restrict__ dp, int B) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const float* d = dh + 8 * (size_t)b;
+    dp[3 * b] = d[0];
+    dp[3 * b + 1] = d[1];
+    dp[3 * b + 2] = d[3] - d[2];
+}
+
 }  // namespace marf
 
 // ------------------------------------------------------------------ launch helpers (C++)
+
+hipError_t marf_launch_se2_embed(const float* p, float* h, int B, hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(marf::k_se2_to_sl3, dim3((B + 63) / 64), dim3(64), 0, s, p, h, B);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_se2_embed_bwd(const float* dh, float* dp, int B, hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(marf::k_se2_to_sl3_bwd, dim3((B + 63) / 64), dim3(64), 0, s, dh, dp, B);
+    return hipGetLastError();
+}
 
 hipError_t marf_launch_sl3(const float* h, float* H, int B, int batch_hint, hipStream_t s) {
     if (B <= 0) return hipSuccess;

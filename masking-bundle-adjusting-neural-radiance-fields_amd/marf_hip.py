@@ -34,6 +34,8 @@ _SIGS = {
     "marf_version": (_c_int, []),
     "marf_sl3_to_SL3": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_vp]),
     "marf_sl3_to_SL3_backward": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp]),
+    "marf_se2_to_sl3": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp]),
+    "marf_se2_to_sl3_backward": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp]),
     "marf_pixel_grid": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_vp, _c_vp]),
     "marf_warp_points": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp]),
     "marf_posenc": (_c_int, [_c_vp, _c_ll, _c_int, ctypes.POINTER(C2f), _c_vp, _c_vp]),
@@ -173,6 +175,34 @@ def sl3_to_SL3(h, lie_batch=0):
     hb = h.reshape(-1, 8)
     lb = lie_batch if lie_batch > 0 else hb.shape[0]
     return _SL3.apply(hb, lb).reshape(*shp, 3, 3)
+
+
+class _SE2Embed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, p):
+        p = _f32(p, "p")
+        h = torch.empty(p.shape[0], 8, device=p.device, dtype=torch.float32)
+        _check(lib().marf_se2_to_sl3(_ptr(p), _ptr(h), p.shape[0], _stream(p)))
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        dh = _f32(dh, "dh")
+        dp = torch.empty(dh.shape[0], 3, device=dh.device, dtype=torch.float32)
+        _check(lib().marf_se2_to_sl3_backward(_ptr(dh), _ptr(dp), dh.shape[0], _stream(dh)))
+        return dp
+
+
+def se2_to_sl3(p):
+    """se(2) tangent p [..., 3] = (tx, ty, theta) -> the sl(3) parameters [..., 8] of the same
+    generator (an extension: the reference has no SE(2), warp.py:72-80), differentiable."""
+    shp = p.shape[:-1]
+    return _SE2Embed.apply(p.reshape(-1, 3)).reshape(*shp, 8)
+
+
+def se2_to_SE2(p, lie_batch=0):
+    """p [..., 3] -> the SE(2) matrix [..., 3, 3] (the sl(3) exponential of the embedded generator)."""
+    return sl3_to_SL3(se2_to_sl3(p), lie_batch)
 
 
 def pixel_grid(H, W, patch_H, patch_W, crop, device):

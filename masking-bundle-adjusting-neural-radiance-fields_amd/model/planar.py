@@ -217,6 +217,8 @@ class Model(torch.nn.Module):
         return rgb.view(self.opt.H, self.opt.W, 3).detach().cpu().permute(2, 0, 1)
 
     def homography_error(self, pred_hom, gt_hom):
+        if self.opt.warp.type == "se2":
+            pred_hom = marf_hip.se2_to_sl3(pred_hom)
         pred_h = self.lie.sl3_to_SL3(pred_hom)
         return torch.norm((pred_h - gt_hom) ** 2).mean()
 
@@ -290,12 +292,21 @@ class Graph(torch.nn.Module):
         self.it = 0
         if opt.use_implicit_mask:
             raise NotImplementedError("the implicit-mask branch is outside this implementation")
-        if opt.warp.type != "homography" or opt.warp.dof != 8:
-            raise AssertionError("only the 8-dof sl(3) homography warp exists (warp.py:72-80)")
+        # warp.py:72-80 has the 8-dof sl(3) homography only; "se2" (3 dof: tx, ty, theta) is this
+        # implementation's extension (north_star "sl(3)/SE(2)"): its generator is embedded in the
+        # sl(3) parameters on the GPU (marf_hip.se2_to_sl3), so every kernel path is shared
+        if (opt.warp.type, opt.warp.dof) not in (("homography", 8), ("se2", 3)):
+            raise AssertionError(f"warp {opt.warp.type} with {opt.warp.dof} dof: homography / 8 (warp.py:72-80) "
+                                 "or se2 / 3 (extension)")
         self.shard = None
         self.loss_denominator = None
         self.edge_denominator = None
         self.need_edges = True
+
+    def warp_h(self):
+        """The warps as the reference's sl(3) parameters [B, 8] (se2: the embedded generators)."""
+        w = self.warp_param.weight
+        return marf_hip.se2_to_sl3(w) if self.opt.warp.type == "se2" else w
 
     def set_shard(self, rank, world, images):
         """Own patches [rank*B/world, (rank+1)*B/world); the masked-MSE denominator 3*sum(mask)
@@ -327,10 +338,10 @@ class Graph(torch.nn.Module):
             # computed in the same pass (marf_step_forward); compute_loss picks the loss up
             masks = imgs.masks[b0:b1] if imgs.get("masks") is not None else None
             denom = self.loss_denominator if self.shard is not None else None
-            rgb, loss_rgb = self.neural_image.render_step(self.warp_param.weight, imgs.rgb[b0:b1], masks, denom, b0, b1)
+            rgb, loss_rgb = self.neural_image.render_step(self.warp_h(), imgs.rgb[b0:b1], masks, denom, b0, b1)
             var.fused_loss = (loss_rgb, imgs.rgb, imgs.get("masks"))
         else:
-            rgb = self.neural_image.render(self.warp_param.weight, b0, b1)  # [Bl, h*w, 3]
+            rgb = self.neural_image.render(self.warp_h(), b0, b1)  # [Bl, h*w, 3]
         var.rgb_prediction = rgb
         var.rgb_prediction_map = rgb.view(b1 - b0, int(self.h), int(self.w), 3).permute(0, 3, 1, 2)
         if self.opt.use_edges and self.need_edges:

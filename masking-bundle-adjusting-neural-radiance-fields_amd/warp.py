@@ -4,6 +4,7 @@
   Warp(opt).warp_grid(xy_grid, warp)         -> [B, N, 2]        (HIP Lie exp + warp kernels, autograd)
   Warp(opt).warp_corners(warp_param)         -> [B, 4, 2]
   Lie().sl3_to_SL3(h)                        -> [..., 3, 3]      (HIP, torch.matrix_exp bit-exact)
+  Lie().se2_to_SE2(p)                        -> [..., 3, 3]      (extension: se(2) tangent (tx, ty, theta))
 
 The training forward does not call these: Graph.forward runs grid, warp, posenc and MLP fused in
 one kernel (marf_hip.render_train).  These entry points exist for drop-in callers and logging.
@@ -40,10 +41,14 @@ class Warp:
         return xy.unsqueeze(0).expand(self.batch_size, -1, -1)  # [B, HW, 2] (broadcast view)
 
     def warp_grid(self, xy_grid, warp):
-        if self.warp_type != "homography":
+        if self.warp_type == "homography":
+            assert self.dof == 8
+            H = lie.sl3_to_SL3(warp)  # differentiable: HIP matrix_exp adjoint
+        elif self.warp_type == "se2":  # extension (the reference has no SE(2) warp)
+            assert self.dof == 3
+            H = lie.se2_to_SE2(warp)
+        else:
             raise AssertionError(f"unsupported warp type {self.warp_type}")
-        assert self.dof == 8
-        H = lie.sl3_to_SL3(warp)  # differentiable: HIP matrix_exp adjoint
         return marf_hip.warp_points(xy_grid, H)  # differentiable in xy and H
 
     def warp_corners(self, warp_param):
@@ -60,6 +65,10 @@ class Warp:
 class Lie:
     def sl3_to_SL3(self, h):
         return marf_hip.sl3_to_SL3(h)
+
+    def se2_to_SE2(self, p):
+        """se(2) tangent (tx, ty, theta) -> SE(2) (extension; exp of the embedded sl(3) generator)."""
+        return marf_hip.se2_to_SE2(p)
 
 
 lie = Lie()
