@@ -495,6 +495,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         uint32_t bits, mw;
         float vp, xo;
         uint32_t hw[8], lw[8];
+        float ta, tb;  // split pack in two halves: the f32 values of the hi pair
     } ep;
     f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
     // forward step e: ReLU + mask bit of register e (frelu); the odd steps then pack the (hi, lo)
@@ -545,6 +546,43 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 ep.hw[e >> 1] = w;
             }
         }
+    };
+    // the split pack in two halves (the same operations as fpack): A = the hi pair and its f32
+    // values, B = the lo pair (the remainders); B of a pair must precede the next frelu (it reads
+    // the pair's values, which the next even step overwrites)
+    auto fpackA = [&](auto ec) {
+        constexpr int e = decltype(ec)::value;
+        static_assert(e & 1, "odd step");
+#ifdef S2_DIAG_NOEPI
+        return;
+#endif
+        uint32_t w;
+        float t0, t1;
+        asm volatile(
+            "v_cvt_pk_bf16_f32 %0, %3, %4\n\t"
+            "v_lshlrev_b32_e32 %1, 16, %0\n\t"
+            "v_and_b32_e32 %2, 0xffff0000, %0"
+            : "=&v"(w), "=&v"(t0), "=&v"(t1)
+            : "v"(ep.vp), "v"(ep.xo));
+        ep.hw[e >> 1] = w;
+        ep.ta = t0;
+        ep.tb = t1;
+    };
+    auto fpackB = [&](auto ec) {
+        constexpr int e = decltype(ec)::value;
+        static_assert(e & 1, "odd step");
+#ifdef S2_DIAG_NOEPI
+        return;
+#endif
+        uint32_t wl;
+        float r0, r1;
+        asm volatile(
+            "v_sub_f32_e32 %1, %3, %5\n\t"
+            "v_sub_f32_e32 %2, %4, %6\n\t"
+            "v_cvt_pk_bf16_f32 %0, %1, %2"
+            : "=&v"(wl), "=&v"(r0), "=&v"(r1)
+            : "v"(ep.vp), "v"(ep.xo), "v"(ep.ta), "v"(ep.tb));
+        ep.lw[e >> 1] = wl;
     };
     auto fstep = [&](const f32x16& pa, auto ec) {
         frelu(pa, ec);
@@ -702,6 +740,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             auto fwd_layer = [&](int l, const S2Frag* Bhi, const S2Frag* Blo, int nk, auto nk_tag, auto ms_tag) {
                 constexpr int MS = decltype(ms_tag)::value;  // epilogue micro-steps beside each k-step
                 typedef std::integral_constant<bool, decltype(nk_tag)::value == NKH> PcL;  // hidden: pieces in the GEMM
+                constexpr bool SPLITPK = SPLIT && MS == 1 && decltype(nk_tag)::value == NKH;  // hidden, split recipe
                 const int nrt = ly_int(l, 0);
                 const bool save = l + 1 < nl - 1 && !a.fwd_only;
                 u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) + 8 * h : nullptr;
@@ -729,15 +768,28 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                             ep.bits = 0;
                             S2T_BEGIN(8);
                             gemm(cur, slot, Bhi, Blo, nk, MFt(), nk_tag, [&](auto ksc, auto pc) {
-                                s2_sfor<MS>([&](auto jc) {
-                                    constexpr int e = decltype(ksc)::value * MS + decltype(jc)::value;
-                                    if constexpr (e < 16) {
-                                        if constexpr (decltype(pc)::value == 0) frelu(prv, std::integral_constant<int, e>());
-                                        else fpack(std::integral_constant<int, e>());
+                                constexpr int ks = decltype(ksc)::value, p = decltype(pc)::value;
+                                if constexpr (SPLITPK) {
+                                    // one step per k-step, the pack of pair (ks-1, ks) split over the
+                                    // second gap of ks and the first gap of ks+1 (balanced gaps)
+                                    if constexpr (p == 0) {
+                                        if constexpr ((ks & 1) == 0 && ks >= 2) fpackB(std::integral_constant<int, ks - 1>());
+                                        frelu(prv, ksc);
+                                    } else if constexpr (ks & 1) {
+                                        fpackA(ksc);
                                     }
-                                });
+                                } else {
+                                    s2_sfor<MS>([&](auto jc) {
+                                        constexpr int e = ks * MS + decltype(jc)::value;
+                                        if constexpr (e < 16) {
+                                            if constexpr (p == 0) frelu(prv, std::integral_constant<int, e>());
+                                            else fpack(std::integral_constant<int, e>());
+                                        }
+                                    });
+                                }
                             }, PcL());
                             S2T_END(8);
+                            if constexpr (SPLITPK) fpackB(std::integral_constant<int, 15>());
                             s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
                                 if (decltype(ec)::value >= MS * nk) fstep(prv, ec);
                             });
