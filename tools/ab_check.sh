@@ -1,5 +1,7 @@
 #!/bin/bash
-# Bit-for-bit A/B of the step kernel against a reference build (lib/libmarf_old.so), then a short
+# Bit-for-bit A/B of the step kernel against a reference build (lib/libmarf_old.so, e.g. built from
+# the last commit:  git archive HEAD <pkg>/csrc <pkg>/build_lib.py include | tar -x -C /tmp/old &&
+# (cd /tmp/old/<pkg> && python build_lib.py --variant libmarf_old.so), copied into lib/), then a short
 # bench of the current build.  bash tools/ab_check.sh <tag>
 set -o pipefail
 TAG=${1:-ab}
