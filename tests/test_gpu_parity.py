@@ -180,7 +180,8 @@ def test_small_step_fp32_vs_reference(tag, tmp_path):
             assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max() + 1e-12, (tag, i, name)
     ref = z[f"{tag}_grad0_warp_param.weight"]
     got = m.graph.warp_param.weight.grad.cpu().numpy()
-    assert np.abs(got - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-12
+    # fp32 contract 1e-5 relative to the max (measured <= 2.7e-7 on the four cases)
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max() + 1e-12
 
 
 @pytest.mark.parametrize("tag", SMALL)
@@ -247,7 +248,9 @@ def test_c1_real_init_and_trajectory_fp32(tmp_path):
             np.testing.assert_allclose(rgb, z["rgb0"], atol=1e-5)  # fp32 1e-5
             np.testing.assert_allclose(float(loss.rgb), 0.050604186952114105, rtol=1e-6)
             dh = m.graph.warp_param.weight.grad.cpu().numpy()
-            np.testing.assert_allclose(dh, z["grad0_warp"], atol=1e-4 * np.abs(z["grad0_warp"]).max())
+            # fp32 contract 1e-5 relative to the max (measured 9.6e-6: a 5x8 reduction over 216,000
+            # pixels in another fp32 summation order; deterministic, so the value is fixed)
+            np.testing.assert_allclose(dh, z["grad0_warp"], atol=1e-5 * np.abs(z["grad0_warp"]).max())
         m.graph.warp_param.weight.data[0] = 0
         losses.append(float(loss.rgb))
     np.testing.assert_allclose(losses, z["loss"], rtol=1e-5)
@@ -961,8 +964,10 @@ def test_homography_error_vs_reference(tmp_path):
 
 def test_c1_L10_steps_vs_reference(tmp_path):
     """BASELINE config 1 as written (L=10): cat_batch3, seed 3, 4 training iterations against the
-    reference.  rgb <= 1e-5 abs, loss <= 1e-5 rel, d warp <= 1e-4 relative to its max (a 5x8
-    reduction over 216,000 pixels in a different fp32 order), warps after 4 Adam steps <= 1e-5."""
+    reference.  rgb <= 1e-5 abs, loss <= 1e-5 rel, d warp <= 2e-5 relative to its max (measured
+    1.5e-5: a 5x8 reduction over 216,000 pixels in a different fp32 order -- at C3 such sums are
+    bounded against float64 by 2x the reference's own fp32 error, _compare_step), warps after 4
+    Adam steps <= 1e-5."""
     z = g("step_c1_L10")
     from model import planar
     from util import EasyDict as edict
@@ -989,8 +994,7 @@ def test_c1_L10_steps_vs_reference(tmp_path):
             got = var.rgb_prediction.detach().cpu().numpy().reshape(-1, 3)[z["rgb0_idx"]]
             np.testing.assert_allclose(got, z["rgb0"], atol=1e-5)
             dh = m.graph.warp_param.weight.grad.cpu().numpy()
-            print("L10 dh rel err", np.abs(dh - z["grad0_warp"]).max() / np.abs(z["grad0_warp"]).max())
-            np.testing.assert_allclose(dh, z["grad0_warp"], atol=1e-4 * np.abs(z["grad0_warp"]).max())
+            np.testing.assert_allclose(dh, z["grad0_warp"], atol=2e-5 * np.abs(z["grad0_warp"]).max())
         m.graph.warp_param.weight.data[0] = 0
         losses.append(float(loss.rgb))
     np.testing.assert_allclose(losses, z["loss"], rtol=1e-5)
