@@ -301,7 +301,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     // c_stage - 1 (burst: issue it now)
     auto stage_begin = [&](bool burst) -> const char* {
         S2T_BEGIN(0);
+        S2T_BEGIN(12);
         wait_ring();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        S2T_END(12);
         st_prev = st_cur;
         st_cur = 0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -743,7 +746,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 constexpr bool SPLITPK = SPLIT && MS == 1 && decltype(nk_tag)::value == NKH;  // hidden, split recipe
                 const int nrt = ly_int(l, 0);
                 const bool save = l + 1 < nl - 1 && !a.fwd_only;
+#ifdef S2_DIAG_CONTIG  // timing only: each store 1 KB contiguous (wrong layout; results invalid)
+                u16* srow = save ? ly_ptr(l + 1, 0) + (myslot - pxl) * ly_int(l + 1, 3) + 8 * lane : nullptr;
+#else
                 u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) + 8 * h : nullptr;
+#endif
                 const int boff = ly_int(l, 2);
                 const char* slot0 = nullptr;
                 s2_sfor<NRT>([&](auto rtc) {
@@ -957,7 +964,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const int nrt = ly_int(nl - 1, 1);
             u16* brow[NS];
             s2_sfor<NS>([&](auto sc) {
+#ifdef S2_DIAG_CONTIG
+                brow[decltype(sc)::value] = ly_ptr(nl - 1, 1) + (myslot_of(decltype(sc)::value) - pxl) * ly_int(nl - 1, 4) + 8 * lane;
+#else
                 brow[decltype(sc)::value] = ly_ptr(nl - 1, 1) + myslot_of(decltype(sc)::value) * ly_int(nl - 1, 4) + 8 * h;
+#endif
             });
             S2Frag gB[NS];
             s2_sfor<NS>([&](auto sc) { gB[decltype(sc)::value] = ss[decltype(sc)::value].g; });
@@ -1008,7 +1019,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const int nrt = ly_int(l, 1);
             u16* brow[NS];
             s2_sfor<NS>([&](auto sc) {
+#ifdef S2_DIAG_CONTIG
+                brow[decltype(sc)::value] = ly_ptr(l, 1) + (myslot_of(decltype(sc)::value) - pxl) * ly_int(l, 4) + 8 * lane;
+#else
                 brow[decltype(sc)::value] = ly_ptr(l, 1) + myslot_of(decltype(sc)::value) * ly_int(l, 4) + 8 * h;
+#endif
             });
             s2_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;
