@@ -303,7 +303,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         S2T_BEGIN(0);
         S2T_BEGIN(12);
         wait_ring();
+#ifdef MARF_STAMPS  // (the stamp splits the vm / lgkm wait from the barrier)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
         S2T_END(12);
         st_prev = st_cur;
         st_cur = 0;
