@@ -339,8 +339,6 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
         return fail(MARF_ERR_UNSUPPORTED, "net_create: hidden width %d > 512", hmax);
     }
     n->TP = (n->kdt == 1 && n->Kmax <= 256) ? 128 : 64;
-    if (const char* e = getenv("MARF_STEP_TP"))  // diagnostic: bf16 tile width override (64 / 128)
-        if (n->kdt == 1 && (atoi(e) == 64 || atoi(e) == 128)) n->TP = atoi(e);
     n->lda = n->kdt == 1 ? n->Kmax + 8 : n->Kmax + 1;
     size_t act = (size_t)n->TP * n->lda * n->elem;
     size_t df = (size_t)n->TP * (n->Kp[0] + 1) * 4;
