@@ -16,7 +16,8 @@
  *   - Every function returns 0 on success or a negative MARF_ERR_* code; marf_last_error()
  *     returns a thread-local message for the last failure.
  *   - float32 everywhere in the interface; dtype selects the internal MLP arithmetic
- *     (MARF_FP32 = exact fp32 MFMA, MARF_BF16 = bf16 MFMA with fp32 accumulation).
+ *     (MARF_FP32 = exact fp32 MFMA, MARF_BF16 = bf16 MFMA with fp32 accumulation, MARF_BF16X3 = split
+ *     bf16, MARF_FP16 = fp16 MFMA with fp32 accumulation).
  */
 #ifndef MARF_H
 #define MARF_H
@@ -36,7 +37,11 @@ extern "C" {
 #define MARF_FP32 0
 #define MARF_BF16 1
 #define MARF_BF16X3 2 /* split bf16: weights and forward activations as bf16 hi + lo pairs (hi*hi + hi*lo + lo*hi
-                         forward, hi + lo weights in the dgrad), bf16 dz / saved tensors; fused step only */
+                         forward, hi + lo weights in the dgrad), bf16 dz / saved tensors; fused step and
+                         marf_render only (marf_forward / marf_backward return MARF_ERR_UNSUPPORTED) */
+
+#define MARF_FP16 3   /* fp16 MFMA (v_mfma_f32_32x32x16_f16, fp32 accumulation): weights, activations, dz and the
+                         saved tensors in IEEE binary16 (11 significant bits); the bf16 rate */
 
 #define MARF_GEO_GRID 0   /* pixels of the centre crop, warped by a per-patch homography */
 #define MARF_GEO_COORDS 1 /* explicit [n][2] coordinates (one point set) */
@@ -63,6 +68,9 @@ typedef struct {
 
 const char* marf_last_error(void);
 int marf_version(void);
+/* sha1 of the sources the library was built from (build_lib.py embeds it; the host binding refuses
+ * a library whose hash differs from the sources next to it). */
+const char* marf_source_hash(void);
 
 /* ---- Lie group (warp.py:95-106 Lie.sl3_to_SL3; torch.linalg.matrix_exp semantics).
  * lie_batch: the batch size torch would see (selects torch's path; pass B unless sharded). */

@@ -3,8 +3,11 @@
     python build_lib.py [--force]
     python build_lib.py --variant libmarf_<name>.so "<extra hipcc flags>"   (A/B variants, MARF_LIB=...)
 
-The library is rebuilt when any source under csrc/ or include/ is newer than it.
+The library is rebuilt when any source under csrc/ or include/ is newer than it.  Every build
+embeds a hash of those sources (marker MARF_SOURCE_HASH=<sha1>); marf_hip.lib() compares it with
+the sources next to it before loading, so an out-of-date binary is never loaded silently.
 """
+import hashlib
 import glob
 import os
 import subprocess
@@ -19,6 +22,27 @@ SOURCES = ["marf_lie.hip", "marf_mlp.hip", "marf_wgrad.hip", "marf_step.hip", "m
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          # exact fp32 operation order for the bit-exact prologue (no implicit FMA contraction)
          "-ffp-contract=off", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function"]
+
+
+def source_hash():
+    """sha1 over the names and contents of csrc/* and include/*.h (what every build compiles)."""
+    h = hashlib.sha1()
+    deps = sorted(glob.glob(os.path.join(HERE, "csrc", "*")) + glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for d in deps:
+        h.update(os.path.relpath(d, ROOT).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def embedded_hash(lib_path):
+    """The source hash a built library carries (None if it has no marker)."""
+    with open(lib_path, "rb") as f:
+        data = f.read()
+    i = data.find(b"MARF_SOURCE_HASH=")
+    if i < 0:
+        return None
+    return data[i + 17:i + 57].decode(errors="replace")
 
 
 def _stale():
@@ -50,18 +74,24 @@ def _compile(lib_path, extra, verbose):
         print("[marf] building", lib_path, flush=True)
     jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
     with tempfile.TemporaryDirectory() as td:
-        objs, procs = [], []
-        cflags = [f for f in FLAGS if f != "-shared"]
+        objs, procs, logs = [], [], []
+        cflags = [f for f in FLAGS if f != "-shared"] + [f'-DMARF_SOURCE_HASH="{source_hash()}"']
         for src in SOURCES:
             obj = os.path.join(td, src.replace(".hip", ".o"))
             objs.append(obj)
+            # compiler output to a file, not a pipe: a pipe nobody drains blocks a verbose compile
+            log = open(obj + ".log", "w+")
+            logs.append(log)
             procs.append(subprocess.Popen([hipcc] + cflags + extra + ["-c", os.path.join(HERE, "csrc", src), "-o", obj],
-                                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+                                          stdout=log, stderr=subprocess.STDOUT))
             while sum(p.poll() is None for p in procs) >= jobs:
                 procs[[p.poll() is None for p in procs].index(True)].wait()
         errs = []
-        for src, p in zip(SOURCES, procs):
-            out = p.communicate()[0]
+        for src, p, log in zip(SOURCES, procs, logs):
+            p.wait()
+            log.seek(0)
+            out = log.read()
+            log.close()
             if p.returncode != 0:
                 errs.append(f"{src}:\n{out}")
         if errs:

@@ -53,7 +53,7 @@ struct Step2NetPlan {
 
 struct marf_net {
     int n_layers, L, D, dtype;
-    int kdt;  // kernel arithmetic of the generic kernels: 0 fp32, 1 bf16 (MARF_BF16 and MARF_BF16X3)
+    int kdt;  // kernel arithmetic of the generic kernels: 0 fp32, 1 bf16 (MARF_BF16 and MARF_BF16X3), 2 fp16
     Step2NetPlan s2;
     int dims[MARF_MAX_LAYERS + 1];
     int Kp[MARF_MAX_LAYERS], Mp[MARF_MAX_LAYERS], Mt[MARF_MAX_LAYERS];
@@ -80,6 +80,9 @@ static void plan_step2_net(marf_net* n) {
     if (n->kdt != 1 || nl < 2 || nl > 5 || n->L > 32) return;
     for (int l = 0; l < nl - 1; ++l)
         if (n->Mp[l] > 256) return;
+    // decided once, here: the split recipe always runs this kernel; plain bf16 only on request
+    // (MARF_STEP2=1 at net creation), otherwise it runs the tile kernel and needs no program
+    if (n->dtype != MARF_BF16X3 && !step2_env_enabled()) return;
     q.HM = 256;
     q.variant = n->dtype == MARF_BF16X3 ? 1 : 0;
     {
@@ -124,6 +127,13 @@ const char* marf_last_error(void) { return g_err.c_str(); }
 // Diagnostic builds only: device buffer [n_tiles][32] for the fused step's phase stamps.
 void marf_debug_set_stamps(void* d_stamps) { g_stamps = (unsigned long long*)d_stamps; }
 int marf_version(void) { return 1; }
+
+#ifndef MARF_SOURCE_HASH
+#define MARF_SOURCE_HASH "0000000000000000000000000000000000000000"
+#endif
+// the marker is searched for in the binary by build_lib.embedded_hash
+static const char k_source_hash[] = "MARF_SOURCE_HASH=" MARF_SOURCE_HASH;
+const char* marf_source_hash(void) { return k_source_hash + 17; }
 
 // ------------------------------------------------------------------ Lie / warp / posenc
 
@@ -301,7 +311,7 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
     *out = nullptr;
     if (n_layers < 2 || n_layers > MARF_MAX_LAYERS)
         return fail(MARF_ERR_UNSUPPORTED, "net_create: n_layers=%d (supported 2..%d)", n_layers, MARF_MAX_LAYERS);
-    if (dtype != MARF_FP32 && dtype != MARF_BF16 && dtype != MARF_BF16X3)
+    if (dtype != MARF_FP32 && dtype != MARF_BF16 && dtype != MARF_BF16X3 && dtype != MARF_FP16)
         return fail(MARF_ERR_INVALID, "net_create: dtype %d", dtype);
     if (L < 0 || L > 32) return fail(MARF_ERR_UNSUPPORTED, "net_create: L=%d (supported 0..32)", L);
     int D = L > 0 ? 2 + 4 * L : 2;
@@ -313,8 +323,8 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
     n->L = L;
     n->D = D;
     n->dtype = dtype;
-    n->kdt = dtype == MARF_FP32 ? 0 : 1;
-    n->elem = n->kdt == 1 ? 2 : 4;
+    n->kdt = dtype == MARF_FP32 ? 0 : (dtype == MARF_FP16 ? 2 : 1);
+    n->elem = n->kdt != 0 ? 2 : 4;
     for (int i = 0; i <= n_layers; ++i) {
         if (dims[i] <= 0) {
             delete n;
@@ -331,15 +341,15 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
         hmax = std::max(hmax, n->Mp[l]);
     }
     n->Mp[n_layers - 1] = 16;
-    n->Mt[n_layers - 1] = n->kdt == 1 ? 16 : 4;
+    n->Mt[n_layers - 1] = n->kdt != 0 ? 16 : 4;
     n->Kmax = 0;
     for (int l = 0; l < n_layers; ++l) n->Kmax = std::max(n->Kmax, n->Kp[l]);
     if (hmax > 512 || n->Kmax > 512) {
         delete n;
         return fail(MARF_ERR_UNSUPPORTED, "net_create: hidden width %d > 512", hmax);
     }
-    n->TP = (n->kdt == 1 && n->Kmax <= 256) ? 128 : 64;
-    n->lda = n->kdt == 1 ? n->Kmax + 8 : n->Kmax + 1;
+    n->TP = (n->kdt != 0 && n->Kmax <= 256) ? 128 : 64;
+    n->lda = n->kdt != 0 ? n->Kmax + 8 : n->Kmax + 1;
     size_t act = (size_t)n->TP * n->lda * n->elem;
     size_t df = (size_t)n->TP * (n->Kp[0] + 1) * 4;
     n->lds_fwd = act;
@@ -531,6 +541,8 @@ size_t marf_workspace_bytes(const marf_net* net, const marf_geometry* geo) {
 int marf_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
                  float* d_rgb, void* d_saved, void* stream) {
     if (!net || !d_packed || !d_rgb) return fail(MARF_ERR_INVALID, "forward: NULL argument");
+    if (net->dtype == MARF_BF16X3)  // the generic kernels have no split-bf16 arithmetic
+        return fail(MARF_ERR_UNSUPPORTED, "forward: split-bf16 nets run marf_step_forward / marf_render only");
     FwdArgs a;
     memset(&a, 0, sizeof(a));
     int rc = make_geo(geo, a.geo, MARF_TILE_PAD);
@@ -560,6 +572,8 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
                   void* stream) {
     if (!net || !d_packed || !d_rgb_out || !d_drgb || !d_saved || !d_workspace)
         return fail(MARF_ERR_INVALID, "backward: NULL argument");
+    if (net->dtype == MARF_BF16X3)
+        return fail(MARF_ERR_UNSUPPORTED, "backward: split-bf16 nets run marf_step_backward only");
     hipStream_t s = (hipStream_t)stream;
     BwdArgs a;
     memset(&a, 0, sizeof(a));
@@ -704,11 +718,7 @@ static int device_cus() {
     return cus[dev];
 }
 
-static bool use_step2(const marf_net* n) {
-    if (n->s2.variant < 0) return false;
-    if (n->s2.variant != 1 && !step2_env_enabled()) return false;
-    return true;
-}
+static bool use_step2(const marf_net* n) { return n->s2.variant >= 0; }
 
 // render = a forward-only launch: no saved tensors, no dH / weight-gradient partials
 static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p, bool render = false) {

@@ -26,6 +26,7 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
@@ -53,6 +54,9 @@ MARF_DEV u16 f2bf(float x) {
     return __builtin_bit_cast(u16, b);
 }
 MARF_DEV float bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
+// fp16 (IEEE binary16): v_cvt_f16_f32 / v_cvt_pk_f16_f32, round-to-nearest-even
+MARF_DEV u16 f2h(float x) { return __builtin_bit_cast(u16, static_cast<_Float16>(x)); }
+MARF_DEV float h2f(u16 h) { return static_cast<float>(__builtin_bit_cast(_Float16, h)); }
 // diagnostic builds: round an fp32-path value to bf16 precision (numerics experiments)
 MARF_DEV float diag_round_bf16(float x) { return bf2f(f2bf(x)); }
 MARF_DEV float diag_round_fp16(float x) { return (float)(_Float16)x; }
@@ -94,6 +98,39 @@ struct PrecBF16 {
     }
     MARF_DEV static T cvt(float x) { return f2bf(x); }
     MARF_DEV static float tof(T x) { return bf2f(x); }
+    MARF_DEV static uint32_t pk2(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        return __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){a, b}), bf16x2));
+    }
+};
+
+// fp16: v_mfma_f32_32x32x16_f16 / 16x16x32_f16, the bf16 forms' shapes, fragment layouts and
+// rate, with 11 significant bits per operand instead of 8 (MARF_FP16).
+struct PrecF16 {
+    typedef u16 T;
+    static constexpr int KS = 16;
+    static constexpr int KS16 = 32;
+    static constexpr int FE = 8;
+    typedef f16x8 frag;
+    static constexpr int kDtype = 2;
+
+    MARF_DEV static frag load_frag(const T* p) { return *reinterpret_cast<const frag*>(p); }
+    MARF_DEV static int kofs(int lane) { return 8 * (lane >> 5); }
+    MARF_DEV static int kofs16(int lane) { return 8 * (lane >> 4); }
+    MARF_DEV static f32x16 mma32(frag a, frag b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+    MARF_DEV static f32x4 mma16(frag a, frag b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+    MARF_DEV static T cvt(float x) { return f2h(x); }
+    MARF_DEV static float tof(T x) { return h2f(x); }
+    MARF_DEV static uint32_t pk2(float a, float b) {  // one v_cvt_pk_f16_f32 (RNE)
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+        return __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){a, b}), f16x2));
+    }
 };
 
 // fp32: v_mfma_f32_32x32x2_f32 (exact fp32 fma chain). Lane l holds A[row l&31][k0 + (l>>5)],

@@ -267,12 +267,10 @@ MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
 // Store 4 consecutive rows (features) of one accumulator group for this lane's pixel.
 template <class P>
 MARF_DEV void store4(typename P::T* dst, float x0, float x1, float x2, float x3) {
-    if (sizeof(typename P::T) == 2) {
-        typedef float f32x2 __attribute__((ext_vector_type(2)));
-        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-        uint2 v;  // one v_cvt_pk_bf16_f32 per pair (RNE)
-        v.x = __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){x0, x1}), bf16x2));
-        v.y = __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){x2, x3}), bf16x2));
+    if constexpr (sizeof(typename P::T) == 2) {
+        uint2 v;  // one packed RNE conversion per pair
+        v.x = P::pk2(x0, x1);
+        v.y = P::pk2(x2, x3);
         *reinterpret_cast<uint2*>(dst) = v;
     } else {
         float* d = reinterpret_cast<float*>(dst);
@@ -329,10 +327,7 @@ MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, co
     T* row = act + (size_t)i * lda;
     auto put2 = [&](int col, float a0, float a1) {  // col even
         if constexpr (sizeof(T) == 2) {
-            typedef float f32x2 __attribute__((ext_vector_type(2)));
-            typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-            *reinterpret_cast<uint32_t*>(row + col) =
-                __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){a0, a1}), bf16x2));
+            *reinterpret_cast<uint32_t*>(row + col) = P::pk2(a0, a1);
         } else {
             row[col] = a0;
             row[col + 1] = a1;
@@ -467,8 +462,10 @@ MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
             for (int r = 0; r < 16; ++r) {
                 const int m = __builtin_amdgcn_sbfe((int)w, 16 * (1 - (ti & 1)) + 15 - r, 1);
                 o[r] = __int_as_float(__float_as_int(acc[i][j][r]) & m);
-#ifdef MARF_DIAG_DZ_BF16
+#if defined(MARF_DIAG_DZ_BF16)
                 o[r] = diag_round_bf16(o[r]);
+#elif defined(MARF_DIAG_DZ_FP16)
+                o[r] = diag_round_fp16(o[r]);
 #endif
             }
 #pragma unroll

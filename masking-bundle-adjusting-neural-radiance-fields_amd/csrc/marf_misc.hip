@@ -166,6 +166,8 @@ __global__ void k_pack(const float* __restrict__ params, char* __restrict__ pack
             float wtv = m < L.M && kr < L.K ? W[(size_t)m * L.K + kr] : 0.f;
 #if defined(MARF_DIAG_WT_BF16)
             wtv = diag_round_bf16(wtv);
+#elif defined(MARF_DIAG_WT_FP16)
+            wtv = diag_round_fp16(wtv);
 #endif
             wt[e - nf] = P::cvt(wtv);
         } else {
@@ -368,6 +370,8 @@ hipError_t marf_launch_pack(int dtype, const float* params, char* packed, const 
     dim3 grid(grid_for(max_elems), a.n_layers);
     if (dtype == 1)
         hipLaunchKernelGGL(k_pack<PrecBF16>, grid, dim3(256), 0, s, params, packed, a);
+    else if (dtype == 2)
+        hipLaunchKernelGGL(k_pack<PrecF16>, grid, dim3(256), 0, s, params, packed, a);
     else
         hipLaunchKernelGGL(k_pack<PrecF32>, grid, dim3(256), 0, s, params, packed, a);
     return hipGetLastError();

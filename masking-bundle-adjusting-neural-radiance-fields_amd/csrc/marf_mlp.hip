@@ -192,10 +192,12 @@ static hipError_t launch_bwd_t(const BwdArgs& a, size_t lds, int n_tiles, hipStr
 
 hipError_t marf_launch_mlp_fwd(const FwdArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s) {
     if (dtype == 1) return TP == 128 ? launch_fwd_t<PrecBF16, 128>(a, lds, n_tiles, s) : launch_fwd_t<PrecBF16, 64>(a, lds, n_tiles, s);
+    if (dtype == 2) return TP == 128 ? launch_fwd_t<PrecF16, 128>(a, lds, n_tiles, s) : launch_fwd_t<PrecF16, 64>(a, lds, n_tiles, s);
     return TP == 128 ? launch_fwd_t<PrecF32, 128>(a, lds, n_tiles, s) : launch_fwd_t<PrecF32, 64>(a, lds, n_tiles, s);
 }
 
 hipError_t marf_launch_mlp_bwd(const BwdArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s) {
     if (dtype == 1) return TP == 128 ? launch_bwd_t<PrecBF16, 128>(a, lds, n_tiles, s) : launch_bwd_t<PrecBF16, 64>(a, lds, n_tiles, s);
+    if (dtype == 2) return TP == 128 ? launch_bwd_t<PrecF16, 128>(a, lds, n_tiles, s) : launch_bwd_t<PrecF16, 64>(a, lds, n_tiles, s);
     return TP == 128 ? launch_bwd_t<PrecF32, 128>(a, lds, n_tiles, s) : launch_bwd_t<PrecF32, 64>(a, lds, n_tiles, s);
 }

@@ -256,13 +256,13 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
                 const int g = lane >> 4, gi = lane & 15;
 #pragma unroll
                 for (int k0 = 0; k0 < TP; k0 += 32) {
-                    bf16x8 fa;
-                    if (gi < 8) fa = *reinterpret_cast<const bf16x8*>(&gT[gi][k0 + 8 * g]);
-                    else fa = (bf16x8){};
+                    typename P::frag fa;
+                    if (gi < 8) fa = *reinterpret_cast<const typename P::frag*>(&gT[gi][k0 + 8 * g]);
+                    else fa = (typename P::frag){};
                     const int r0 = k0 + 8 * g + (gi >> 2);
                     const u16* base = reinterpret_cast<const u16*>(act) + (size_t)r0 * lda + ct * 16 + 4 * (gi & 3);
                     i16x4 v[2] = {tr_read16(base), tr_read16(base + 4 * lda)};
-                    acc = P::mma16(fa, *reinterpret_cast<bf16x8*>(v), acc);
+                    acc = P::mma16(fa, *reinterpret_cast<typename P::frag*>(v), acc);
                 }
             } else {
                 const int kk = lane >> 4, n = lane & 15;
@@ -290,7 +290,11 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         const int i = threadIdx.x;
         T* row = act + (size_t)i * lda;
         const int Kt = net.Mt[nl - 1];
+#if defined(MARF_DIAG_DZ_FP16)  // numerics experiment: the last-layer dgrad operand in fp16
+        for (int c = 0; c < Kt; ++c) row[c] = P::cvt(c < 3 ? diag_round_fp16(gl[i][c]) : 0.f);
+#else
         for (int c = 0; c < Kt; ++c) row[c] = P::cvt(c < 3 ? gl[i][c] : 0.f);
+#endif
     }
     STAMP(10);
     __syncthreads();
@@ -379,6 +383,7 @@ static hipError_t launch_step_b(const StepArgs& a, size_t lds, int n_tiles, hipS
 
 hipError_t marf_launch_mlp_step(const StepArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s) {
     if (dtype == 1) return TP == 128 ? launch_step_b<PrecBF16, 128>(a, lds, n_tiles, s) : launch_step_b<PrecBF16, 64>(a, lds, n_tiles, s);
+    if (dtype == 2) return TP == 128 ? launch_step_b<PrecF16, 128>(a, lds, n_tiles, s) : launch_step_b<PrecF16, 64>(a, lds, n_tiles, s);
     return TP == 128 ? launch_step_b<PrecF32, 128>(a, lds, n_tiles, s) : launch_step_b<PrecF32, 64>(a, lds, n_tiles, s);
 }
 

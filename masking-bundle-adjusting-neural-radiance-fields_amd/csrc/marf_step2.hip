@@ -16,16 +16,17 @@
 //     (issued by every wave, 1 KB per instruction) two stages ahead of its use.  The block is
 //     persistent (one per CU) and the per-tile stage sequence repeats, so the stream never stops
 //     between pixel tiles.
-//   * ReLU masks stay in registers from the forward to the backward (no mask records in HBM).
+//   * the ReLU masks of the forward are packed into one word per lane per pair of row tiles and
+//     kept in wave-private LDS until the dgrad pass reads them (no mask records in HBM).
 //   * split-bf16 mode (MARF_BF16X3): weights and forward activations are carried as bf16 hi + lo
 //     pairs, the forward is hi*hi + hi*lo + lo*hi (fp32 accumulation, ~16 significant bits) and
 //     the dgrad is W_hi^T dz + W_lo^T dz; dz and the saved tensors stay bf16.  This is the precision
 //     recipe that keeps the seed-3 planar run in the reference's basin.
 //
 // Memory ordering: all global traffic inside the tile loop is inline asm (LDS-DMA, stores) so the
-// compiler inserts no vmcnt waits of its own; every stage issues exactly ST store instructions
-// (padding with stores to a per-wave scratch line), so the wait for a ring slot is one constant
-// vmcnt (D * ST + (D - 1) * PER_DMA younger operations).
+// compiler inserts no vmcnt waits of its own.  Each wave counts the store instructions it issues
+// per stage (st_cur / st_prev), and the wait for a ring slot is the vmcnt that leaves exactly the
+// operations younger than that slot's DMA in flight (wait_ring).
 #include <type_traits>
 
 #include "marf_args.h"
@@ -1373,7 +1374,8 @@ static hipError_t launch_step2_t(const Step2Args& a, int grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-// variant: 0 = bf16 256-wide (8 waves), 1 = split 256-wide (4 waves), 2 = bf16 512-wide (4 waves)
+// variant: 0 = plain bf16, 256-wide, 8 waves; 1 = split bf16, 256-wide, 4 waves; 2 = plain bf16,
+// 256-wide, 4 waves (diagnostic: the variant-0 arithmetic at one wave per SIMD)
 hipError_t marf_launch_step2(const Step2Args& a, int variant, int grid, hipStream_t s) {
     switch (variant) {
         case 0: return launch_step2_t<256, false, 8, 4>(a, grid, s);

@@ -132,7 +132,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
                     const u16* base = reinterpret_cast<const u16*>(tz) + r0 * LDZ + c0;
                     i16x4 lo = tr_read(base), hi = tr_read(base + 4 * LDZ);
                     i16x4 v[2] = {lo, hi};
-                    af[i] = *reinterpret_cast<bf16x8*>(v);
+                    af[i] = *reinterpret_cast<typename P::frag*>(v);
                 }
 #pragma unroll
                 for (int j = 0; j < CT; ++j) {
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
                     const u16* base = reinterpret_cast<const u16*>(tf) + r0 * LDF + c0;
                     i16x4 lo = tr_read(base), hi = tr_read(base + 4 * LDF);
                     i16x4 v[2] = {lo, hi};
-                    bf[j] = *reinterpret_cast<bf16x8*>(v);
+                    bf[j] = *reinterpret_cast<typename P::frag*>(v);
                 }
 #pragma unroll
                 for (int i = 0; i < RT; ++i)
@@ -229,7 +229,7 @@ MARF_DEV int foff(int r, int c) {
     else return r * (KF * 2) + c * 2;
 }
 
-template <int NBUF, int SP, int KF>
+template <class P, int NBUF, int SP, int KF>
 __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     static_assert(KF == 256 || KF == 96, "feat width");
     constexpr int WR = KF == 256 ? 4 : 8, WC = 8 / WR;  // wave grid over the 256 x KF output
@@ -323,29 +323,29 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
 #pragma unroll
             for (int r = 0; r < SP; r += 2) {
                 const int rr = r + (threadIdx.x >> 8);
-                bsum += bf2f(*reinterpret_cast<const u16*>(tz + swz(rr, c)));
+                bsum += P::tof(*reinterpret_cast<const u16*>(tz + swz(rr, c)));
             }
         }
 #pragma unroll
         for (int ks = 0; ks < SP; ks += 16) {
             const int r0 = ks + 8 * (g >> 1) + q4;  // rows r0 and r0 + 4 (same r & 3)
-            PrecBF16::frag af[RT], bf[CT];
+            typename P::frag af[RT], bf[CT];
 #pragma unroll
             for (int i = 0; i < RT; ++i) {
                 const u16* base = reinterpret_cast<const u16*>(tz + swz(r0, (wr * RT + i) * 32 + 16 * (g & 1) + 4 * p4));
                 i16x4 v[2] = {tr_read(base), tr_read(base + 4 * 256)};
-                af[i] = *reinterpret_cast<bf16x8*>(v);
+                af[i] = *reinterpret_cast<typename P::frag*>(v);
             }
 #pragma unroll
             for (int j = 0; j < CT; ++j) {
                 const u16* base = reinterpret_cast<const u16*>(tf + foff<KF>(r0, (wc * CT + j) * 32 + 16 * (g & 1) + 4 * p4));
                 i16x4 v[2] = {tr_read(base), tr_read(base + 4 * KF)};
-                bf[j] = *reinterpret_cast<bf16x8*>(v);
+                bf[j] = *reinterpret_cast<typename P::frag*>(v);
             }
 #pragma unroll
             for (int i = 0; i < RT; ++i)
 #pragma unroll
-                for (int j = 0; j < CT; ++j) acc[i][j] = PrecBF16::mma32(af[i], bf[j], acc[i][j]);
+                for (int j = 0; j < CT; ++j) acc[i][j] = P::mma32(af[i], bf[j], acc[i][j]);
         }
     }
 
@@ -541,7 +541,7 @@ static bool wgrad_dma_enabled() {
 #define MARF_WG_NBUF_0 4
 #endif
 
-template <int KF>
+template <class P, int KF>
 static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
     a.n_chunks = n_chunks;
     a.n_oblk_c = a.K / KF;
@@ -549,10 +549,10 @@ static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
     constexpr int NBUF = KF == 256 ? MARF_WG_NBUF_H : MARF_WG_NBUF_0;  // ring depth within 160 KB of LDS
     const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024);
     {
-        hipError_t e = ensure_dynamic_lds((const void*)k_wgrad_dma<NBUF, SP, KF>, lds);
+        hipError_t e = ensure_dynamic_lds((const void*)k_wgrad_dma<P, NBUF, SP, KF>, lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((k_wgrad_dma<NBUF, SP, KF>), dim3(n_chunks * (a.M / 256) * a.n_oblk_c), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((k_wgrad_dma<P, NBUF, SP, KF>), dim3(n_chunks * (a.M / 256) * a.n_oblk_c), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 
@@ -579,16 +579,25 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
     int BM = cfg == 2 ? 128 : 256, BN = cfg == 0 ? 256 : (cfg == 3 ? 128 : 64);
     int nr = (M + BM - 1) / BM, nc = (K + BN - 1) / BN;
     a.n_oblk_c = nc;
+    // LDS-DMA ring: 256-wide dz with a 256-wide (hidden) or 96-wide (layer 0, L = 16) feat
+    const bool dma = M % 256 == 0 && ldz % 8 == 0 && ldz >= M && S % 32 == 0 && chunk % 32 == 0 &&
+                     (long long)n_chunks * (M / 256) * ((K + 255) / 256) <= 0x7fffffff && wgrad_dma_enabled();
+    const bool dma256 = dma && K % 256 == 0 && ldf % 8 == 0 && ldf >= K, dma96 = dma && K == 96 && ldf == 96;
     if (dtype == 1) {
-        // LDS-DMA ring: 256-wide dz with a 256-wide (hidden) or 96-wide (layer 0, L = 16) feat
-        const bool dma = M % 256 == 0 && ldz % 8 == 0 && ldz >= M && S % 32 == 0 && chunk % 32 == 0 &&
-                         (long long)n_chunks * (M / 256) * ((K + 255) / 256) <= 0x7fffffff && wgrad_dma_enabled();
-        if (dma && K % 256 == 0 && ldf % 8 == 0 && ldf >= K) return launch_wg_dma<256>(a, n_chunks, s);
-        if (dma && K == 96 && ldf == 96) return launch_wg_dma<96>(a, n_chunks, s);
+        if (dma256) return launch_wg_dma<PrecBF16, 256>(a, n_chunks, s);
+        if (dma96) return launch_wg_dma<PrecBF16, 96>(a, n_chunks, s);
         if (cfg == 0) return launch_wg<PrecBF16, 2, 4>(a, n_chunks, nr * nc, s);
         if (cfg == 3) return launch_wg<PrecBF16, 2, 2>(a, n_chunks, nr * nc, s);
         if (cfg == 1) return launch_wg<PrecBF16, 2, 1>(a, n_chunks, nr * nc, s);
         return launch_wg<PrecBF16, 1, 1>(a, n_chunks, nr * nc, s);
+    }
+    if (dtype == 2) {
+        if (dma256) return launch_wg_dma<PrecF16, 256>(a, n_chunks, s);
+        if (dma96) return launch_wg_dma<PrecF16, 96>(a, n_chunks, s);
+        if (cfg == 0) return launch_wg<PrecF16, 2, 4>(a, n_chunks, nr * nc, s);
+        if (cfg == 3) return launch_wg<PrecF16, 2, 2>(a, n_chunks, nr * nc, s);
+        if (cfg == 1) return launch_wg<PrecF16, 2, 1>(a, n_chunks, nr * nc, s);
+        return launch_wg<PrecF16, 1, 1>(a, n_chunks, nr * nc, s);
     }
     if (cfg == 0) return launch_wg<PrecF32, 2, 4>(a, n_chunks, nr * nc, s);
     if (cfg == 3) return launch_wg<PrecF32, 2, 2>(a, n_chunks, nr * nc, s);
@@ -600,6 +609,9 @@ hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* fea
                                   int n_chunks, float* partial, float* bpartial, hipStream_t s) {
     if (dtype == 1)
         hipLaunchKernelGGL(k_wgrad_last<PrecBF16>, dim3(n_chunks), dim3(256), 0, s, glast, feat, S, ldf, K, chunk,
+                           partial, bpartial);
+    else if (dtype == 2)
+        hipLaunchKernelGGL(k_wgrad_last<PrecF16>, dim3(n_chunks), dim3(256), 0, s, glast, feat, S, ldf, K, chunk,
                            partial, bpartial);
     else
         hipLaunchKernelGGL(k_wgrad_last<PrecF32>, dim3(n_chunks), dim3(256), 0, s, glast, feat, S, ldf, K, chunk,

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MARF_LIB selects a diagnostic build (lib/libmarf_stamps.so, tools/phase_stamps.py)
 LIB_PATH = os.environ.get("MARF_LIB") or os.path.join(_HERE, "lib", "libmarf.so")
 
-MARF_FP32, MARF_BF16, MARF_BF16X3 = 0, 1, 2
+MARF_FP32, MARF_BF16, MARF_BF16X3, MARF_FP16 = 0, 1, 2, 3
 GEO_GRID, GEO_COORDS, GEO_CANVAS = 0, 1, 2
 
 _c_int, _c_ll, _c_dbl, _c_vp, _c_sz = ctypes.c_int, ctypes.c_longlong, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
@@ -32,6 +32,7 @@ class C2f(ctypes.Structure):
 _SIGS = {
     "marf_last_error": (ctypes.c_char_p, []),
     "marf_version": (_c_int, []),
+    "marf_source_hash": (ctypes.c_char_p, []),
     "marf_sl3_to_SL3": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_vp]),
     "marf_sl3_to_SL3_backward": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp]),
     "marf_se2_to_sl3": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp]),
@@ -80,16 +81,30 @@ _lib = None
 PARAM_GENERATION = [0]
 
 
+def _ensure_current():
+    """Refuse (or, for the default library, rebuild) a libmarf.so whose embedded source hash does
+    not match the sources next to it (build_lib.source_hash)."""
+    import build_lib
+    default = not os.environ.get("MARF_LIB")
+    want = build_lib.source_hash()
+    have = build_lib.embedded_hash(LIB_PATH) if os.path.exists(LIB_PATH) else None
+    if have == want:
+        return
+    if not default:
+        raise RuntimeError(f"libmarf: {LIB_PATH} was built from other sources (hash {have}, sources {want}); "
+                           "rebuild it (build_lib.py --variant)")
+    try:
+        build_lib.build(force=True, verbose=False)
+    except Exception as e:  # pragma: no cover - message path
+        raise RuntimeError(f"libmarf.so at {LIB_PATH} is missing or stale and could not be built: {e}") from e
+
+
 def lib():
-    """Load libmarf.so (building it first if the sources are newer and hipcc is present)."""
+    """Load libmarf.so; a library built from other sources than the ones in this tree is rebuilt
+    (default path) or refused (MARF_LIB variants), never loaded silently."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            try:
-                import build_lib
-                build_lib.build(verbose=False)
-            except Exception as e:  # pragma: no cover - message path
-                raise RuntimeError(f"libmarf.so not found at {LIB_PATH} and could not be built: {e}") from e
+        _ensure_current()
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)

@@ -37,7 +37,9 @@ def _precision(opt):
         return marf_hip.MARF_BF16
     if p in ("bf16x3", "split-bf16"):
         return marf_hip.MARF_BF16X3
-    raise ValueError(f"precision must be fp32, bf16 or bf16x3, got {p}")
+    if p in ("fp16", "float16", "half"):
+        return marf_hip.MARF_FP16
+    raise ValueError(f"precision must be fp32, fp16, bf16 or bf16x3, got {p}")
 
 
 def _dist():
@@ -370,6 +372,10 @@ class Graph(torch.nn.Module):
                         # this rank's share of the global masked MSE: the per-rank terms sum to it
                         diff = (var.edge_prediction - imgs.edges[b0:b1]) * me
                         edge_loss = (diff ** 2).sum() / self.edge_denominator
+                    elif self.shard is not None and me is None:
+                        # unmasked: this rank's share of the global mean over all B patches
+                        diff = var.edge_prediction - imgs.edges[b0:b1]
+                        edge_loss = (diff ** 2).sum() / (self.batch_size * diff[0].numel())
                     else:
                         edge_loss = self.mse_loss(var.edge_prediction, imgs.edges[b0:b1], me)
                 else:  # edges are evaluated at logging steps only (they carry no gradient)
