@@ -63,7 +63,25 @@ struct marf_net {
     int TP, lda, Kmax;
     size_t lds_fwd, lds_bwd, lds_step;
     int elem;  // bytes per stored element
+    unsigned diag[MARF_MAX_LAYERS];  // numerics-experiment rounding codes (MARF_DIAG_PREC; MARF_DIAG_RT builds)
 };
+
+// MARF_DIAG_PREC = "WTAD,WTAD,..." per layer (digits: marf_common.h diag_round modes; the last entry
+// repeats): the rounding a lower-precision recipe would apply, emulated by the fp32 kernels of a
+// MARF_DIAG_RT build (tools/recipe_sweep.sh).  Read once at net creation; other builds ignore it.
+static void parse_diag(marf_net* n) {
+    const char* e = getenv("MARF_DIAG_PREC");
+    unsigned code = 0;
+    for (int l = 0; l < n->n_layers; ++l) {
+        if (e && *e) {
+            code = 0;
+            for (int k = 0; k < 4 && e[k] >= '0' && e[k] <= '9'; ++k) code |= (unsigned)(e[k] - '0') << (4 * k);
+            while (*e && *e != ',') ++e;
+            if (*e == ',') ++e;
+        }
+        n->diag[l] = code;
+    }
+}
 
 static bool step2_env_enabled() {
     const char* e = getenv("MARF_STEP2");  // plain bf16 on the pixel-per-wave kernel: opt-in ("1")
@@ -375,6 +393,7 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
     }
     n->param_count = off;
     n->packed_bytes = boff;
+    parse_diag(n);
     plan_step2_net(n);
     if (n->s2.variant >= 0) n->packed_bytes = n->s2.end_off;
     if (dtype == MARF_BF16X3 && n->s2.variant < 0) {
@@ -408,6 +427,7 @@ int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, vo
         p.wf_off = net->wf_off[l];
         p.wt_off = net->wt_off[l];
         p.bias_off = net->bias_off[l];
+        p.diag = net->diag[l];
         mx = std::max(mx, (long long)p.Mp * p.Kp + (long long)p.Kp * p.Mt + p.Mp);
     }
     MarfProfScope ps("pack_weights", (hipStream_t)stream);
@@ -456,6 +476,7 @@ static void fill_netdev(const marf_net* n, const void* packed, NetDev& d) {
         d.Wf[l] = (const char*)packed + n->wf_off[l];
         d.Wt[l] = (const char*)packed + n->wt_off[l];
         d.bias[l] = (const float*)((const char*)packed + n->bias_off[l]);
+        d.diag[l] = n->diag[l];
     }
 }
 

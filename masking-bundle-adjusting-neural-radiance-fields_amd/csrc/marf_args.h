@@ -63,6 +63,7 @@ struct PackLayer {
     int Mp, Kp, Mt;                      // padded: Wf [Mp][Kp], Wt [Kp][Mt], bias [Mp]
     long long w_off, b_off;              // offsets in the flat fp32 parameter vector
     long long wf_off, wt_off, bias_off;  // byte offsets in the packed buffer
+    unsigned diag;                       // numerics-experiment rounding code (marf_common.h)
 };
 
 struct PackArgs {

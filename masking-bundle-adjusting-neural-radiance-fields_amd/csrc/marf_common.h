@@ -57,20 +57,29 @@ MARF_DEV float bf2f(u16 h) { return __uint_as_float(((uint32_t)h) << 16); }
 // fp16 (IEEE binary16): v_cvt_f16_f32 / v_cvt_pk_f16_f32, round-to-nearest-even
 MARF_DEV u16 f2h(float x) { return __builtin_bit_cast(u16, static_cast<_Float16>(x)); }
 MARF_DEV float h2f(u16 h) { return static_cast<float>(__builtin_bit_cast(_Float16, h)); }
-// diagnostic builds: round an fp32-path value to bf16 precision (numerics experiments)
-MARF_DEV float diag_round_bf16(float x) { return bf2f(f2bf(x)); }
-MARF_DEV float diag_round_fp16(float x) { return (float)(_Float16)x; }
-// a value carried as a bf16 hi + lo pair (~16 significant bits: what split-bf16 GEMMs see)
-MARF_DEV float diag_round_split(float x) {
-    const float h = bf2f(f2bf(x));
-    return h + bf2f(f2bf(x - h));
+// Numerics experiments (diagnostic builds, -DMARF_DIAG_RT; tools/recipe_sweep.sh): the fp32
+// kernels round chosen operands as a lower-precision recipe would see them.  Per layer l, nibble k
+// of NetDev::diag[l] is the mode of operand class k -- 0 the forward weight W_l, 1 the dgrad
+// weight W_l^T, 2 layer l's input activation, 3 the gradient at layer l's output (dz) -- with mode
+// 0 exact fp32, 1 bf16, 2 bf16 hi + lo (~16 bits), 3 fp16, 4 fp16 hi + lo (~22 bits).
+MARF_DEV float diag_round(float x, int mode) {
+    if (mode == 1) return bf2f(f2bf(x));
+    if (mode == 2) {
+        const float h = bf2f(f2bf(x));
+        return h + bf2f(f2bf(x - h));
+    }
+    if (mode == 3) return h2f(f2h(x));
+    if (mode == 4) {
+        const float h = h2f(f2h(x));
+        return h + h2f(f2h(x - h));
+    }
+    return x;
 }
-#if defined(MARF_DIAG_SPLIT)
-#define DIAG_RND diag_round_split
-#elif defined(MARF_DIAG_ACT_FP16) || defined(MARF_DIAG_FEAT_FP16)
-#define DIAG_RND diag_round_fp16
+MARF_DEV int diag_mode(unsigned code, int k) { return (int)((code >> (4 * k)) & 15u); }
+#ifdef MARF_DIAG_RT
+#define MARF_DIAG_ROUND(x, code, k) diag_round((x), diag_mode((code), (k)))
 #else
-#define DIAG_RND diag_round_bf16
+#define MARF_DIAG_ROUND(x, code, k) (x)
 #endif
 
 // ------------------------------------------------------------------ precision traits
@@ -173,6 +182,7 @@ struct NetDev {
     const void* Wf[MARF_MAX_LAYERS];  // packed forward weights (T)
     const void* Wt[MARF_MAX_LAYERS];  // packed transposed weights (T)
     const float* bias[MARF_MAX_LAYERS];  // padded fp32 bias [Mp]
+    unsigned diag[MARF_MAX_LAYERS];      // numerics-experiment rounding codes (MARF_DIAG_RT builds)
 };
 
 // Geometry of the pixel source.

@@ -33,11 +33,7 @@ MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int col
     } else {
         for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
             int r = e / cols, c = e - r * cols;
-#if defined(MARF_DIAG_SAVE_BF16)
-            dst[(size_t)r * ldd + c] = diag_round_bf16(act[(size_t)r * lda + c]);
-#else
             dst[(size_t)r * ldd + c] = act[(size_t)r * lda + c];
-#endif
         }
     }
 }
@@ -333,11 +329,7 @@ MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, co
             row[col + 1] = a1;
         }
     };
-#if defined(MARF_DIAG_FEAT_BF16) || defined(MARF_DIAG_FEAT_FP16)
-    if (part == NPART - 1) put2(0, DIAG_RND(u), DIAG_RND(v));
-#else
-    if (part == NPART - 1) put2(0, u, v);
-#endif
+    if (part == NPART - 1) put2(0, MARF_DIAG_ROUND(u, net.diag[0], 2), MARF_DIAG_ROUND(v, net.diag[0], 2));
     if (L > 0) {
         const int c = part / HALF, sub = part - c * HALF;
         const float cv = c ? v : u;
@@ -351,10 +343,8 @@ MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, co
                 sv = sv * w;
                 cvv = cvv * w;
             }
-#if defined(MARF_DIAG_FEAT_BF16) || defined(MARF_DIAG_FEAT_FP16)
-            sv = DIAG_RND(sv);
-            cvv = DIAG_RND(cvv);
-#endif
+            sv = MARF_DIAG_ROUND(sv, net.diag[0], 2);
+            cvv = MARF_DIAG_ROUND(cvv, net.diag[0], 2);
         };
         if ((k & 1) && k < k1) {  // odd start: single band
             float s0, c0;
@@ -404,7 +394,8 @@ MARF_DEV uint4* mask_record(uint64_t* mk, int tile, int wave, int lane) {
 // v_cndmask (relu), v_addc (shift the bit into the tile's mask word).
 template <class P, int RT, int PT>
 MARF_DEV void relu_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, int n_rt, int wave, int lane,
-                            uint64_t* mk, int tile) {
+                            uint64_t* mk, int tile, unsigned diag_next = 0) {
+    (void)diag_next;  // (the next layer's rounding code: MARF_DIAG_RT builds)
     uint32_t words[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
@@ -428,9 +419,7 @@ MARF_DEV void relu_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
                     : "v"(acc[i][j][r])
                     : "vcc");
                 o[r] = v;
-#if defined(MARF_DIAG_ACT_BF16) || defined(MARF_DIAG_ACT_FP16)
-                o[r] = DIAG_RND(o[r]);
-#endif
+                o[r] = MARF_DIAG_ROUND(o[r], diag_next, 2);
             }
             words[ti >> 1] |= bits << (16 * (1 - (ti & 1)));
 #pragma unroll
@@ -445,7 +434,8 @@ MARF_DEV void relu_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
 // written to act.  Per element: v_bfe_i32 (0 / -1 from the bit) and v_and.
 template <class P, int RT, int PT>
 MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, int n_rt, int wave, int lane,
-                            uint4 mw) {
+                            uint4 mw, unsigned diag_out = 0) {
+    (void)diag_out;  // (the rounding code of the layer whose output gradient this is: MARF_DIAG_RT)
     const uint32_t words[4] = {mw.x, mw.y, mw.z, mw.w};
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
@@ -462,11 +452,7 @@ MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
             for (int r = 0; r < 16; ++r) {
                 const int m = __builtin_amdgcn_sbfe((int)w, 16 * (1 - (ti & 1)) + 15 - r, 1);
                 o[r] = __int_as_float(__float_as_int(acc[i][j][r]) & m);
-#if defined(MARF_DIAG_DZ_BF16)
-                o[r] = diag_round_bf16(o[r]);
-#elif defined(MARF_DIAG_DZ_FP16)
-                o[r] = diag_round_fp16(o[r]);
-#endif
+                o[r] = MARF_DIAG_ROUND(o[r], diag_out, 3);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q)

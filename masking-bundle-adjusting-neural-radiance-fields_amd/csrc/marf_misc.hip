@@ -154,22 +154,12 @@ __global__ void k_pack(const float* __restrict__ params, char* __restrict__ pack
             int m, k;
             frag_coord<P>(e, nkf, last16, m, k);
             float wv = m < L.M && k < L.K ? W[(size_t)m * L.K + k] : 0.f;
-#if defined(MARF_DIAG_W_BF16)
-            wv = DIAG_RND(wv);
-#elif defined(MARF_DIAG_W_FP16)
-            wv = diag_round_fp16(wv);
-#endif
-            wf[e] = P::cvt(wv);
+            wf[e] = P::cvt(MARF_DIAG_ROUND(wv, L.diag, 0));
         } else if (e < nf + nt) {
             int kr, m;  // row of W^T = input feature, column = output feature
             frag_coord<P>(e - nf, nkt, false, kr, m);
             float wtv = m < L.M && kr < L.K ? W[(size_t)m * L.K + kr] : 0.f;
-#if defined(MARF_DIAG_WT_BF16)
-            wtv = diag_round_bf16(wtv);
-#elif defined(MARF_DIAG_WT_FP16)
-            wtv = diag_round_fp16(wtv);
-#endif
-            wt[e - nf] = P::cvt(wtv);
+            wt[e - nf] = P::cvt(MARF_DIAG_ROUND(wtv, L.diag, 1));
         } else {
             int m = (int)(e - nf - nt);
             bias[m] = m < L.M ? bsrc[m] : 0.f;

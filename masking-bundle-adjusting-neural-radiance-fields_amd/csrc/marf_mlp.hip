@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
         f32x16 acc[RT][PT];
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, net.bias[l], st);
         __syncthreads();  // every wave has consumed the layer input
-        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask[l + 1], blockIdx.x);
+        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask[l + 1], blockIdx.x, net.diag[l + 1]);
         __syncthreads();
         st.clear();
         if (a.feat[l + 1]) {
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(BwdArgs a) {
         const uint4 mw = *mask_record(const_cast<uint64_t*>(a.mask[l]), blockIdx.x, wave, lane);
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
         __syncthreads();
-        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, mw);
+        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, mw, net.diag[l - 1]);
         __syncthreads();
         save_tile<P>(st, act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, net.Mt[l - 1] / P::KS);
     }

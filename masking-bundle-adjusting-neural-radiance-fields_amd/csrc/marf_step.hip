@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         boff += M;
         __syncthreads();  // every wave has consumed the layer input
         STAMP(2 + 2 * l);
-        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x);
+        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x, net.diag[l + 1]);
         __syncthreads();
         if (l < 3) STAMP(3 + 2 * l);
         st.clear();
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         const int nk16 = net.Kp[nl - 1] / P::KS16;
 #pragma unroll
         for (int u = 0; u < NWL; ++u) wl[u] = P::load_frag(W + ((size_t)(u < nk16 ? u : 0) * 64 + lane) * P::FE);
-        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x);
+        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x, net.diag[l + 1]);
         __syncthreads();
         st.clear();
     }
@@ -290,11 +290,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         const int i = threadIdx.x;
         T* row = act + (size_t)i * lda;
         const int Kt = net.Mt[nl - 1];
-#if defined(MARF_DIAG_DZ_FP16)  // numerics experiment: the last-layer dgrad operand in fp16
-        for (int c = 0; c < Kt; ++c) row[c] = P::cvt(c < 3 ? diag_round_fp16(gl[i][c]) : 0.f);
-#else
-        for (int c = 0; c < Kt; ++c) row[c] = P::cvt(c < 3 ? gl[i][c] : 0.f);
-#endif
+        for (int c = 0; c < Kt; ++c) row[c] = P::cvt(c < 3 ? MARF_DIAG_ROUND(gl[i][c], net.diag[nl - 1], 3) : 0.f);
     }
     STAMP(10);
     __syncthreads();
@@ -307,7 +303,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         const uint4 mw = *mask_record(a.mask_bits[l], blockIdx.x, wave, lane);  // in flight behind the GEMM
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
         __syncthreads();
-        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, mw);
+        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, mw, net.diag[l - 1]);
         __syncthreads();
         if (l <= 4) STAMP(15 - l);  // 14 .. 11
         save_tile<P>(st, act, lda, TP, R, SAVE_DST(reinterpret_cast<T*>(a.dz[l]) + slot0 * R, R), net.Mt[l - 1] / P::KS);

@@ -233,7 +233,7 @@ class PlanarStep:
     """One Model.train_iteration of the planar graph, restated on the CPU.
 
     cfg keys: H, W, patch_H, patch_W, L (0 = posenc off), c2f (None or [s, e]),
-    max_iter, lr, lr_warp, fix_first, use_edges, alpha_initial, alpha_final.
+    max_iter, lr, lr_warp, fix_first, use_edges, alpha_initial, alpha_final, crop (default True).
     params: list of (W, b) fp32 (modified in place); warp: [B, 8] fp32.
     """
 
@@ -244,7 +244,8 @@ class PlanarStep:
         self.rgb = np.asarray(rgb, np.float32)  # [B,3,h,w]
         self.mask = np.asarray(mask, np.float32)  # [B,1,h,w]
         self.B = self.warp.shape[0]
-        self.xy = pixel_grid(cfg["H"], cfg["W"], cfg["patch_H"], cfg["patch_W"], crop=True)
+        # use_cropped_images off (cfg crop False): every canvas pixel (warp.py:54-68)
+        self.xy = pixel_grid(cfg["H"], cfg["W"], cfg["patch_H"], cfg["patch_W"], crop=cfg.get("crop", True))
         self.h, self.w = self.rgb.shape[2], self.rgb.shape[3]
         self.progress = np.float32(0.0)
         self.it = 0

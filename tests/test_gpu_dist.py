@@ -1,8 +1,9 @@
-"""The patch-sharded data parallelism with the real kernels: two or four processes on the one GPU
-(gloo), each running Model.train_iteration on its shard of the C1 cat_batch3 patches (5 patches ->
-2 + 3, or the ragged 1 + 1 + 1 + 2 that a 512-patch C4 run over 8 GPUs does not hit but a
-non-multiple batch does), against the same iterations in one process.  The sharded sum order of the MLP gradient differs
-(SURVEY.md §8(e)), so the contract is <= 1e-5 relative, not bitwise."""
+"""The patch-sharded data parallelism with the real kernels, on the one GPU (gloo): two or four
+processes, each running Model.train_iteration on its shard of the C1 cat_batch3 patches (5 patches
+-> 2 + 3, or the ragged 1 + 1 + 1 + 2), and eight processes on BASELINE config 4's partition (512
+patches, 64 per rank, at a reduced crop), against the same iterations in one process.  The sharded
+sum order of the MLP gradient differs, so the contract is <= 1e-5 relative, not
+bitwise."""
 import os
 import socket
 
@@ -23,7 +24,12 @@ def _free_port():
     return p
 
 
-def _run(rank, world, port, precision, out):
+# BASELINE config 4's partition (512 patches over 8 ranks = 64 per rank) at a reduced crop: 16x16
+# crops of a 32x32 canvas, the C3/C4 network (L = 16, 66-256x4-3), synthetic seeded targets
+C4_PATCHES, C4_CROP = 512, 16
+
+
+def _run(rank, world, port, precision, out, config="c1"):
     import sys
     import time
     from conftest import GOLDEN, PKG, ROOT
@@ -36,16 +42,24 @@ def _run(rank, world, port, precision, out):
         import options
         from model import planar
         from util import EasyDict as edict
-        imgs = np.load(os.path.join(GOLDEN, "cat_batch3_c1.npz"))
+        over = {"model": "planar", "yaml": "planar", "seed": 3, "barf_c2f": [0, 0.4], "precision": precision}
+        if config == "c4":
+            over.update(H=2 * C4_CROP, W=2 * C4_CROP, patch_H=C4_CROP, patch_W=C4_CROP, batch_size=C4_PATCHES,
+                        arch={"layers": [None, 256, 256, 256, 256, 3], "skip": [], "posenc": {"L_2D": 16}})
         opt = options.load_options("options/planar.yaml")
-        opt = options.override_options(opt, edict({"model": "planar", "yaml": "planar", "seed": 3,
-                                                   "barf_c2f": [0, 0.4], "precision": precision}))
+        opt = options.override_options(opt, edict(over))
         opt.device = "cuda:0"
         opt.output_path = f"/tmp/marf_gpu_dist_{port}_{rank}"
         torch.manual_seed(3)
         m = planar.Model(opt)
-        rgb = torch.from_numpy(imgs["rgb"].astype(np.float32) / np.float32(255)).cuda()
-        mask = torch.from_numpy(imgs["mask"].astype(np.float32)).cuda()
+        if config == "c4":
+            g = np.random.default_rng(0)
+            rgb = torch.from_numpy(g.random((C4_PATCHES, 3, C4_CROP, C4_CROP)).astype(np.float32)).cuda()
+            mask = torch.from_numpy((g.random((C4_PATCHES, 1, C4_CROP, C4_CROP)) < 0.85).astype(np.float32)).cuda()
+        else:
+            imgs = np.load(os.path.join(GOLDEN, "cat_batch3_c1.npz"))
+            rgb = torch.from_numpy(imgs["rgb"].astype(np.float32) / np.float32(255)).cuda()
+            mask = torch.from_numpy(imgs["mask"].astype(np.float32)).cuda()
         m.images = edict(rgb=rgb, masks=mask, masks_eroded=mask, edges=None, gt_hom=None, gt=None)
         m.build_networks()
         m.setup_optimizer()
@@ -57,7 +71,7 @@ def _run(rank, world, port, precision, out):
 
             def __len__(self):
                 return 1
-        var = edict(idx=torch.arange(5), images=m.images)
+        var = edict(idx=torch.arange(opt.batch_size), images=m.images)
         losses, grads = [], None
         for s in range(STEPS):
             loss = m.train_iteration(var, _Loader())
@@ -72,32 +86,37 @@ def _run(rank, world, port, precision, out):
         warps = m.gathered_warps().detach().cpu().numpy()
         params = [p.detach().cpu().numpy().copy() for p in m.graph.neural_image.mlp.parameters()]
         if rank == 0:
-            np.savez(out, losses=np.array(losses), warps=warps, shard=np.array(m.graph.shard or (0, 5)),
+            np.savez(out, losses=np.array(losses), warps=warps, shard=np.array(m.graph.shard or (0, opt.batch_size)),
                      **{f"g{i}": a for i, a in enumerate(grads)}, **{f"p{i}": a for i, a in enumerate(params)})
     finally:
         if world > 1:
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("precision,world", [("fp32", 2), ("bf16x3", 2), ("bf16x3", 4)])
-def test_sharded_step_matches_single(precision, world, tmp_path):
+@pytest.mark.parametrize("precision,world,config", [("fp32", 2, "c1"), ("bf16x3", 2, "c1"), ("bf16x3", 4, "c1"),
+                                                    ("bf16x3", 8, "c4"), ("fp32", 8, "c4")])
+def test_sharded_step_matches_single(precision, world, config, tmp_path):
+    """world 2 / 4 on the C1 batch; world 8 on BASELINE config 4's partition (512 patches, 64 per
+    rank, reduced crop): first-step MLP gradients, losses, and warps / parameters after 3 steps equal
+    the single-process run within 1e-5."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     port = _free_port()
     out2 = str(tmp_path / "sharded.npz")
-    procs = [ctx.Process(target=_run, args=(r, world, port, precision, out2)) for r in range(world)]
+    procs = [ctx.Process(target=_run, args=(r, world, port, precision, out2, config)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
     out1 = str(tmp_path / "one.npz")
-    p1 = ctx.Process(target=_run, args=(0, 1, port, precision, out1))
+    p1 = ctx.Process(target=_run, args=(0, 1, port, precision, out1, config))
     p1.start()
     p1.join(timeout=300)
     assert p1.exitcode == 0
     a, b = np.load(out1), np.load(out2)
-    assert tuple(b["shard"]) == (0, 5 // world)
+    nb = C4_PATCHES if config == "c4" else 5
+    assert tuple(b["shard"]) == (0, nb // world)
     np.testing.assert_allclose(b["losses"], a["losses"], rtol=1e-5)
     n = len([k for k in a.files if k.startswith("g")])
     for i in range(n):  # first-step MLP gradient: <= 1e-5 relative to its max
