@@ -1,6 +1,6 @@
 """Throughput of the planar bundle-adjustment training step on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c1|c5] [--precision bf16x3|bf16|fp32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c1|c5] [--precision bf16x3|bf16|fp16|fp32]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -34,7 +34,7 @@ PEAK_BF16 = 2.5e15   # dense bf16 MFMA, MI355X_MICROARCH.md
 PEAK_FP32 = 157.3e12  # fp32 MFMA = vector rate
 PEAK_HBM = 8.0e12
 RECIPES = {"bf16x3": "bf16x3 recipe (split-bf16 hi+lo MFMA operands, fp32 accumulate; seed-3 parity)",
-           "bf16": "plain bf16 MFMA (fp32 accumulate)", "fp32": "fp32"}
+           "bf16": "plain bf16 MFMA (fp32 accumulate)", "fp16": "plain fp16 MFMA (fp32 accumulate)", "fp32": "fp32"}
 
 CONFIGS = {
     # name: (canvas, crop, patches per GPU, L, hidden layers)
@@ -190,7 +190,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=list(CONFIGS))
-    ap.add_argument("--precision", default=None, choices=["bf16x3", "bf16", "fp32"],
+    ap.add_argument("--precision", default=None, choices=["bf16x3", "bf16", "fp16", "fp32"],
                     help="default bf16x3 (the seed-3 parity recipe); c5's 512-wide layers: bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2f", action="store_true", help="barf_c2f None (BASELINE config 5: c2f on vs off)")

@@ -201,9 +201,12 @@ def test_small_trajectory_fp32_vs_reference(tag, tmp_path):
                                    z[f"{tag}_final_neural_image.mlp.{i}.weight"], atol=1e-5)
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
 @pytest.mark.parametrize("tag", ["a", "c"])
-def test_small_step_bf16(tag, tmp_path):
-    z, m, var, nl = small_setup(tag, "bf16", tmp_path)
+def test_small_step_bf16(tag, precision, tmp_path):
+    """Plain 16-bit MFMA recipes (bf16; fp16 = MARF_FP16, 11 significant bits) against the
+    reference's first step: rgb 1e-2 abs, loss 2e-2 rel, MLP-gradient cosine > 0.99."""
+    z, m, var, nl = small_setup(tag, precision, tmp_path)
     var, loss = one_step_grads(m, var)
     rgb = var.rgb_prediction.detach().cpu().numpy().reshape(z[f"{tag}_rgb0"].shape)
     np.testing.assert_allclose(rgb, z[f"{tag}_rgb0"], atol=1e-2, rtol=0)  # bf16: 1e-2
@@ -268,7 +271,7 @@ def test_c1_real_bf16(tmp_path):
 
 # ------------------------------------------------------------------------ explicit coordinates
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 1e-5), ("bf16", 1e-2)])
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-5), ("bf16", 1e-2), ("fp16", 1e-2)])
 def test_coords_forward_backward_vs_oracle(precision, tol, tmp_path):
     from model.planar import NeuralImageFunction
     opt = make_opt(tmp_path, precision=precision, arch={"layers": [None, 128, 96, 3], "skip": [], "posenc": {"L_2D": 8}})
@@ -299,6 +302,21 @@ def test_coords_forward_backward_vs_oracle(precision, tol, tmp_path):
         # the oracle re-derives (u,v) through an identity warp; compare the coordinate gradient
         np.testing.assert_allclose(c.grad.cpu().numpy().reshape(-1, 2), duv.reshape(-1, 2),
                                    atol=1e-5 * np.abs(duv).max() + 1e-6)
+
+
+def test_split_recipe_refuses_generic_backward(tmp_path):
+    """The split-bf16 recipe exists in the fused step and the render only: a differentiable
+    NeuralImageFunction.forward on a bf16x3 net fails loudly (MARF_ERR_UNSUPPORTED) instead of
+    silently running plain-bf16 arithmetic; without grad it renders in the split recipe."""
+    from model.planar import NeuralImageFunction
+    opt = make_opt(tmp_path, precision="bf16x3", arch={"layers": [None, 128, 96, 3], "skip": [], "posenc": {"L_2D": 8}})
+    torch.manual_seed(0)
+    ni = NeuralImageFunction(opt).to(DEV)
+    c = t(np.random.default_rng(0).uniform(-0.6, 0.6, (1, 300, 2)).astype(np.float32))
+    with torch.no_grad():
+        assert torch.isfinite(ni.forward(c)).all()
+    with pytest.raises(RuntimeError, match="split-bf16"):
+        ni.forward(c.requires_grad_())
 
 
 @pytest.mark.parametrize("n", [1, 127, 129, 1000 + 37])
@@ -357,7 +375,7 @@ def test_masked_mse_vs_oracle():
 
 # ------------------------------------------------------------------------ full-size properties
 
-@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16", "fp16", "fp32"])
 def test_c3_geometry_properties(precision, tmp_path):
     """BASELINE config 3 geometry (256x256 crops of a 512x512 canvas, L=16) at reduced patch count:
     determinism, exact gradient linearity, identity warp, and an oracle spot check."""
@@ -435,7 +453,7 @@ def _grads_of(m):
             m.graph.warp_param.weight.grad.detach().clone())
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("tag", ["a", "c"])
 def test_fused_step_matches_separate_kernels(tag, precision, tmp_path):
     """marf_step_forward/backward (forward + loss + backward in one pass per tile) against the
