@@ -46,11 +46,11 @@ MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int col
 // GEMM has fewer k-steps than the job flush after it.  bf16 tiles only (16-B aligned LDS rows).
 //
 // Wave-uniform walk: rpi = 64 / nch whole rows per wave step (lane -> row lane / nch, chunk
-// lane % nch); wave w copies row groups w, w + 4, ...
+// lane % nch); wave w of nw copies row groups w, w + nw, ...
 template <class T>
 struct TileStore {
     T* dst;
-    int lda, ldd, rows, rpi, q, nq, wave;
+    int lda, ldd, rows, rpi, q, nq, wave, nw;
     int lr, lc;  // per lane
     bool active;
 
@@ -58,7 +58,7 @@ struct TileStore {
         active = false;
         q = nq = 0;
     }
-    MARF_DEV void init(int lda_, T* d, int ldd_, int rows_, int cols, int wave_, int lane) {
+    MARF_DEV void init(int lda_, T* d, int ldd_, int rows_, int cols, int wave_, int lane, int nw_ = 4) {
         constexpr int VEC = 16 / sizeof(T);
         const int nch = cols / VEC;  // <= 64 (cols <= 512)
         dst = d;
@@ -66,16 +66,17 @@ struct TileStore {
         ldd = ldd_;
         rows = rows_;
         wave = wave_;
+        nw = nw_;
         rpi = 64 / nch;
         lr = lane / nch;
         lc = lane - lr * nch;
         q = 0;
-        nq = (rows + 4 * rpi - 1) / (4 * rpi);
+        nq = (rows + nw * rpi - 1) / (nw * rpi);
         active = true;
     }
     MARF_DEV int row() const {
         const int qq = q < nq ? q : nq - 1;
-        const int r = (qq * 4 + wave) * rpi + lr;
+        const int r = (qq * nw + wave) * rpi + lr;
         return r < rows ? r : rows - 1;  // idle lanes / surplus rows repeat the last row's chunk
     }
     MARF_DEV uint4 read(const T* src) const {
@@ -94,15 +95,15 @@ struct TileStore {
     }
 };
 
-// acc[i][PT] += W[rows (wave + 4 i)*32 .., k] . act[px, k]^T over k < K for the NA row tiles this
-// wave owns (i < NA).  NA is dispatched once per layer (wave-uniform), so the body is branch-free.
+// acc[i][PT] += W[rows (wave + NW i)*32 .., k] . act[px, k]^T over k < K for the NA row tiles this
+// wave owns (i < NA; NW waves per block deal the row tiles round-robin).  NA is dispatched once per layer (wave-uniform), so the body is branch-free.
 //
 // Schedule: the weight fragments stream from L2 through a static 4-deep register ring (slot u is
 // reloaded for k-step k+4 right after its MFMAs issue: three k-steps of latency cover, no register
 // moves), the activation fragments of step k+1 are read from LDS while step k's MFMAs run (two
 // statically named buffers).  Loads past the last k-step are clamped to it (harmless L2 hits).
 // JOB: one TileStore chunk per k-step (read before the B prefetch, stored after the A reload).
-template <class P, int NA, int RT, int PT, bool JOB>
+template <class P, int NA, int RT, int PT, bool JOB, int NW = 4>
 MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__ W, int K,
                         const typename P::T* act, int lda, int wave, int lane, TileStore<typename P::T>& st) {
     typedef typename P::frag F;
@@ -112,7 +113,7 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
     // fragment-major weights (marf_common.h): fragment (rt, ks) at ((rt * nk + ks) * 64 + lane) * FE
     const typename P::T* wrow[NA];
 #pragma unroll
-    for (int i = 0; i < NA; ++i) wrow[i] = W + ((size_t)(wave + 4 * i) * nk * 64 + lane) * P::FE;
+    for (int i = 0; i < NA; ++i) wrow[i] = W + ((size_t)(wave + NW * i) * nk * 64 + lane) * P::FE;
     const typename P::T* brow = act + (size_t)rl * lda + ko;
     auto ldA = [&](F (&dst)[NA], int k) {
         const int kc = (k < nk ? k : nk - 1) * 64 * P::FE;
@@ -217,14 +218,14 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
 
 // Accumulators start at the bias of their output row when `bias` is given (so the epilogue does
 // not add it), else at zero.
-template <class P, int RT, int PT>
+template <class P, int RT, int PT, int NW = 4>
 MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__ W, int K, int n_rt,
                         const typename P::T* act, int lda, int wave, int lane, const float* bias,
                         TileStore<typename P::T>& st) {
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
         f32x16 init = (f32x16){};
-        const int rt = wave + 4 * i;
+        const int rt = wave + NW * i;
         if (bias && rt < n_rt) {
             const float* bb = bias + rt * 32 + 4 * (lane >> 5);
 #pragma unroll
@@ -239,22 +240,22 @@ MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
 #pragma unroll
         for (int j = 0; j < PT; ++j) acc[i][j] = init;
     }
-    int na = (n_rt - wave + 3) / 4;
+    int na = (n_rt - wave + NW - 1) / NW;
     na = na < 0 ? 0 : (na > RT ? RT : na);
     if (st.active) {
         switch (na) {
-            case 1: gemm_rows<P, 1, RT, PT, true>(acc, W, K, act, lda, wave, lane, st); break;
-            case 2: gemm_rows<P, 2, RT, PT, true>(acc, W, K, act, lda, wave, lane, st); break;
-            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, true>(acc, W, K, act, lda, wave, lane, st); break;
-            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, true>(acc, W, K, act, lda, wave, lane, st); break;
+            case 1: gemm_rows<P, 1, RT, PT, true, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 2: gemm_rows<P, 2, RT, PT, true, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, true, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, true, NW>(acc, W, K, act, lda, wave, lane, st); break;
             default: st.flush(act); break;
         }
     } else {
         switch (na) {
-            case 1: gemm_rows<P, 1, RT, PT, false>(acc, W, K, act, lda, wave, lane, st); break;
-            case 2: gemm_rows<P, 2, RT, PT, false>(acc, W, K, act, lda, wave, lane, st); break;
-            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, false>(acc, W, K, act, lda, wave, lane, st); break;
-            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, false>(acc, W, K, act, lda, wave, lane, st); break;
+            case 1: gemm_rows<P, 1, RT, PT, false, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 2: gemm_rows<P, 2, RT, PT, false, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, false, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, false, NW>(acc, W, K, act, lda, wave, lane, st); break;
             default: break;
         }
     }
@@ -287,12 +288,12 @@ MARF_DEV void tile_origin(const GeoDev& g, int tile, int TP, int& b, int& p0, lo
 
 // Save the LDS tile to global: bf16 tiles stream during the GEMM that follows (job handed to
 // gemm_tile), fp32 tiles (unaligned LDS rows) are copied right away (job left idle).
-template <class P>
+template <class P, int NW = 4>
 MARF_DEV void save_tile(TileStore<typename P::T>& job, const typename P::T* act, int lda, int rows, int cols,
                         typename P::T* dst, int nk_next) {
     if constexpr (sizeof(typename P::T) == 2) {
         const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        job.init(lda, dst, cols, rows, cols, wave, lane);
+        job.init(lda, dst, cols, rows, cols, wave, lane, NW);
     } else {
         copy_tile_out<P>(act, lda, rows, cols, dst, cols);
         job.clear();
@@ -309,13 +310,13 @@ MARF_DEV void c2f_weights_lds(const C2fDev& c2f, int L, float* wsh) {
 
 // Prologue: pixel grid -> sl(3) warp -> posenc (+c2f) of the tile's TP slots -> act [TP][Kp0]
 // (warp.py:33-81, model/planar.py:451-471; feature layout [u, v, sin_k(u), cos_k(u), sin_k(v),
-// cos_k(v)], zero padded to Kp0).  NPART = 256 / TP threads share a pixel: half of them take u,
+// cos_k(v)], zero padded to Kp0).  NPART = 64 NW / TP threads share a pixel: half of them take u,
 // half v, each a contiguous run of bands, written as bf16 pairs (one 4-byte LDS store per pair).
-template <class P, int TP, bool GRID_ONLY = false>
+template <class P, int TP, bool GRID_ONLY = false, int NW = 4>
 MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh,
                             typename P::T* act, int lda, int b, int p0) {
     typedef typename P::T T;
-    constexpr int NPART = 256 / TP, HALF = NPART / 2;
+    constexpr int NPART = 64 * NW / TP, HALF = NPART / 2;
     const int L = net.L;
     const int i = threadIdx.x % TP, part = threadIdx.x / TP;
     float x, y, u = 0.f, v = 0.f, X[3];
@@ -385,21 +386,22 @@ MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, co
 // ti = i * PT + j (<= 8); tile ti's 16 bits live in word ti >> 1, bits 16 (1 - (ti & 1)) + 15 - r
 // for accumulator register r.  The dgrad epilogue of the backward finds the same (feature, pixel)
 // in the same wave / lane / register (gemm_tile deals row tiles identically for W and W^T).
-MARF_DEV uint4* mask_record(uint64_t* mk, int tile, int wave, int lane) {
-    return reinterpret_cast<uint4*>(mk) + ((size_t)tile * 4 + wave) * 64 + lane;
+MARF_DEV uint4* mask_record(uint64_t* mk, int tile, int wave, int lane, int nw = 4) {
+    return reinterpret_cast<uint4*>(mk) + ((size_t)tile * nw + wave) * 64 + lane;
 }
 
 // Hidden-layer epilogue: ReLU of the accumulators (bias already in them) written back to act in
 // place, and (mk != null) the ReLU mask record of this wave.  Per element: v_cmp (vcc = z > 0),
 // v_cndmask (relu), v_addc (shift the bit into the tile's mask word).
-template <class P, int RT, int PT>
+template <class P, int RT, int PT, int NW = 4>
 MARF_DEV void relu_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, int n_rt, int wave, int lane,
                             uint64_t* mk, int tile, unsigned diag_next = 0) {
+    static_assert(RT * PT <= 8, "a wave's ReLU mask record holds 8 accumulator tiles of 16 bits");
     (void)diag_next;  // (the next layer's rounding code: MARF_DIAG_RT builds)
     uint32_t words[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
-        const int rt = wave + 4 * i;
+        const int rt = wave + NW * i;
         if (rt >= n_rt) continue;
         const int rbase = rt * 32 + 4 * (lane >> 5);
 #pragma unroll
@@ -427,19 +429,20 @@ MARF_DEV void relu_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
                 store4<P>(act + (size_t)px * lda + rbase + 8 * q, o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
         }
     }
-    if (mk) *mask_record(mk, tile, wave, lane) = make_uint4(words[0], words[1], words[2], words[3]);
+    if (mk) *mask_record(mk, tile, wave, lane, NW) = make_uint4(words[0], words[1], words[2], words[3]);
 }
 
 // Dgrad epilogue: dz = acc * relu'(feat) with this wave's mask record `mw` (loaded before the GEMM),
 // written to act.  Per element: v_bfe_i32 (0 / -1 from the bit) and v_and.
-template <class P, int RT, int PT>
+template <class P, int RT, int PT, int NW = 4>
 MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, int n_rt, int wave, int lane,
                             uint4 mw, unsigned diag_out = 0) {
+    static_assert(RT * PT <= 8, "a wave's ReLU mask record holds 8 accumulator tiles of 16 bits");
     (void)diag_out;  // (the rounding code of the layer whose output gradient this is: MARF_DIAG_RT)
     const uint32_t words[4] = {mw.x, mw.y, mw.z, mw.w};
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
-        const int rt = wave + 4 * i;
+        const int rt = wave + NW * i;
         if (rt >= n_rt) continue;
         const int rbase = rt * 32 + 4 * (lane >> 5);
 #pragma unroll
@@ -464,8 +467,8 @@ MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
 // Layer-0 dgrad (d feat_0 = W_0^T dz_1, act holds dz_1) and the posenc / projective-warp adjoint
 // (model/planar.py:451-471, warp.py:74-78 backward): per slot d(u, v), then for the grid geometry
 // d(Hx) and one dH[3x3] partial per tile (fixed-order wave + block sums); for explicit coordinates
-// d coords.  `red` needs 4 * TP * 2 floats, `red9` 4 * 9.  smem = the act tile (reused as fp32).
-template <class P, int TP, bool GRID_ONLY = false>
+// d coords.  `red` needs 64 NW * 2 floats, `red9` NW * 9.  smem = the act tile (reused as fp32).
+template <class P, int TP, bool GRID_ONLY = false, int NW = 4>
 MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh, char* smem, int lda,
                            int wave, int lane, int b, int p0, float* red, float* red9, float* dH_partial,
                            float* d_coords, TileStore<typename P::T>& st, unsigned long long* sp = nullptr) {
@@ -476,14 +479,14 @@ MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, con
     const T* act = reinterpret_cast<const T*>(smem);
     const int R = net.Kp[0], Kk = net.Mt[0], n_rt = R / 32;
     f32x16 acc[RT][PT];
-    gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[0]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
+    gemm_tile<P, RT, PT, NW>(acc, reinterpret_cast<const T*>(net.Wt[0]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
     __syncthreads();
     MARF_STAMP(sp, 16);
     float* df = reinterpret_cast<float*>(smem);
     const int ldf = R + 1;
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
-        const int rt = wave + 4 * i;
+        const int rt = wave + NW * i;
         if (rt >= n_rt) continue;
 #pragma unroll
         for (int j = 0; j < PT; ++j) {
@@ -496,7 +499,7 @@ MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, con
     MARF_STAMP(sp, 17);
 
     // posenc adjoint: d coord_c = df[c] + sum_k w_k f_k (cos(x_k) df_sin - sin(x_k) df_cos)
-    constexpr int NPART = 256 / TP;
+    constexpr int NPART = 64 * NW / TP;
     const int i = threadIdx.x % TP, part = threadIdx.x / TP;
     float x, y, u = 0.f, v = 0.f, X[3] = {0.f, 0.f, 1.f};
     const bool valid = slot_point<GRID_ONLY>(geo, b, p0 + i, x, y, u, v, X);
@@ -563,7 +566,7 @@ MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, con
         __syncthreads();
         if (threadIdx.x < 9) {
             float s = red9[threadIdx.x];
-            for (int w = 1; w < 4; ++w) s += red9[w * 9 + threadIdx.x];
+            for (int w = 1; w < NW; ++w) s += red9[w * 9 + threadIdx.x];
             dH_partial[(size_t)blockIdx.x * 9 + threadIdx.x] = s;
         }
     }
