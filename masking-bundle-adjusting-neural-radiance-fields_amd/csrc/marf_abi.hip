@@ -61,6 +61,7 @@ struct marf_net {
     long long wf_off[MARF_MAX_LAYERS], wt_off[MARF_MAX_LAYERS], bias_off[MARF_MAX_LAYERS];
     size_t packed_bytes;
     int TP, lda, Kmax;
+    int sTP, sNW;  // the fused step's tile (pixel slots) and waves per block (k_mlp_step)
     size_t lds_fwd, lds_bwd, lds_step;
     int elem;  // bytes per stored element
     unsigned diag[MARF_MAX_LAYERS];  // numerics-experiment rounding codes (MARF_DIAG_PREC; MARF_DIAG_RT builds)
@@ -373,6 +374,20 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
     n->lds_fwd = act;
     n->lds_bwd = std::max(act, df);
     n->lds_step = n->lds_bwd;
+    // The fused step of a 16-bit net wider than 256: one 512-thread block per CU at TP = 128
+    // (MARF_STEP_NW=4 at net creation keeps two 4-wave blocks at TP = 64, for A/B runs)
+    n->sTP = n->TP;
+    n->sNW = 4;
+    {
+        const char* e = getenv("MARF_STEP_NW");
+        const bool nw8 = !(e && e[0] == '4');
+        const size_t act8 = (size_t)128 * n->lda * n->elem, df8 = (size_t)128 * (n->Kp[0] + 1) * 4;
+        if (nw8 && n->kdt != 0 && n->Kmax > 256 && std::max(act8, df8) + 16 * 1024 <= 160 * 1024) {
+            n->sTP = 128;
+            n->sNW = 8;
+            n->lds_step = std::max(act8, df8);
+        }
+    }
     if (n->lds_bwd > 160 * 1024) {
         delete n;
         return fail(MARF_ERR_UNSUPPORTED, "net_create: tile does not fit LDS");
@@ -680,7 +695,7 @@ struct StepPlan {
 static void plan_step(const marf_net* n, long long S, StepPlan& p) {
     size_t off = 0;
     const int nl = n->n_layers;
-    p.n_tiles = (int)(S / n->TP);
+    p.n_tiles = (int)(S / n->sTP);
     for (int l = 0; l < nl - 1; ++l) {
         p.feat[l] = off;
         off += rup((long long)S * n->Kp[l] * n->elem, 256);
@@ -690,7 +705,7 @@ static void plan_step(const marf_net* n, long long S, StepPlan& p) {
         p.dz[l] = off;
         off += rup((long long)S * n->Kp[l] * n->elem, 256);
         p.mask[l] = off;
-        off += rup(S / n->TP * 4096, 256);
+        off += rup(S / n->sTP * n->sNW * 1024, 256);  // one uint4 per lane per wave per tile
     }
     p.wlast = off;
     off += rup((long long)p.n_tiles * 3 * n->Kp[nl - 1] * 4, 256);
@@ -1011,7 +1026,7 @@ int marf_step_forward(const marf_net* net, const marf_geometry* geo, const marf_
     if (net->L > 0) HIPCHK(marf_launch_c2f_weights(a.c2f, net->L, (float*)(sv + p.c2f), s), "step_forward c2f");
     {
         MarfProfScope ps("mlp_step", s);
-        HIPCHK(marf_launch_mlp_step(a, net->kdt, net->TP, net->lds_step, p.n_tiles, s), "step_forward");
+        HIPCHK(marf_launch_mlp_step(a, net->kdt, net->sTP, net->sNW, net->lds_step, p.n_tiles, s), "step_forward");
     }
     {
         MarfProfScope ps("loss_final", s);
@@ -1064,7 +1079,7 @@ int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void
     }
     if (d_dh) {
         MarfProfScope ps("warp_bwd", s);
-        HIPCHK(marf_launch_reduce_dH((const float*)(sv + p.dH), g.Np_pad / net->TP, g.B, d_h_params, nullptr, d_dh,
+        HIPCHK(marf_launch_reduce_dH((const float*)(sv + p.dH), g.Np_pad / net->sTP, g.B, d_h_params, nullptr, d_dh,
                                      lie_batch > 0 ? lie_batch : g.B, s, d_gout, denom),
                "step_backward warp");
     }

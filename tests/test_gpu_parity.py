@@ -375,7 +375,7 @@ def test_masked_mse_vs_oracle():
 
 # ------------------------------------------------------------------------ full-size properties
 
-@pytest.mark.parametrize("precision", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_c3_geometry_properties(precision, tmp_path):
     """BASELINE config 3 geometry (256x256 crops of a 512x512 canvas, L=16) at reduced patch count:
     determinism, exact gradient linearity, identity warp, and an oracle spot check."""
