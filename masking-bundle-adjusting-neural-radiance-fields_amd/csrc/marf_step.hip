@@ -165,7 +165,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
             if (u < nk16) {
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
-                    const int px = wave * (TP / 4) + j * 16 + (lane & 15);
+                    const int px = wave * (TP / NW) + j * 16 + (lane & 15);
                     typename P::frag bb = P::load_frag(act + (size_t)px * lda + u * P::KS16 + ko);
                     acc[j] = P::mma16(wl[u], bb, acc[j]);
                 }
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
             typename P::frag wa = P::load_frag(W + ((size_t)u * 64 + lane) * P::FE);
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                const int px = wave * (TP / 4) + j * 16 + (lane & 15);
+                const int px = wave * (TP / NW) + j * 16 + (lane & 15);
                 typename P::frag bb = P::load_frag(act + (size_t)px * lda + u * P::KS16 + ko);
                 acc[j] = P::mma16(wa, bb, acc[j]);
             }
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
             const float* bl = net.bias[nl - 1];
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                const int px = wave * (TP / 4) + j * 16 + lane;
+                const int px = wave * (TP / NW) + j * 16 + lane;
                 const int p = p0 + px;
                 float g[3] = {0.f, 0.f, 0.f};
                 float sq = 0.f, mv = 0.f;

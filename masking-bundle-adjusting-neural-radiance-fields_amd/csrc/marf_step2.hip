@@ -512,17 +512,25 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         return;
 #endif
         // relu as a signed-integer max with 0 (negative floats and -0 are negative integers: exactly
-        // x > 0 ? x : 0), mask bit = (relu(x) != 0), shifted in: no VCC traffic
+        // x > 0 ? x : 0); the mask bits come from the packed bf16 pair (mask_pair)
         float x;
-        uint32_t t;
-        asm volatile(
-            "v_max_i32_e32 %0, 0, %3\n\t"
-            "v_min_u32_e32 %2, 1, %0\n\t"
-            "v_lshl_or_b32 %1, %1, 1, %2"
-            : "=&v"(x), "+v"(ep.bits), "=&v"(t)
-            : "v"(pa[e]));
+        asm volatile("v_max_i32_e32 %0, 0, %1" : "=&v"(x) : "v"(pa[e]));
         if constexpr (e & 1) ep.xo = x;
         else ep.vp = x;
+    };
+    // ReLU mask bits of a packed (relu'd) bf16 pair w: per 16-bit half (w_half != 0), shifted into
+    // ep.bits as two streams -- after the 8 pairs of a row tile the even elements' bits sit at
+    // 7 - j and the odd elements' at 23 - j (pair j).  (w_half != 0) equals z > 0 except for
+    // 0 < z < 2^-134, which rounds to a zero bf16 and would otherwise pass a dz of a feature whose
+    // forward value is a zero hi + a denormal lo: 2 VALU per pair instead of 2 per element.
+    const uint32_t k_pair1 = 0x00010001u;
+    auto mask_pair = [&](uint32_t w) {
+        uint32_t t;
+        asm volatile(
+            "v_pk_min_u16 %1, %2, %3\n\t"
+            "v_lshl_or_b32 %0, %0, 1, %1"
+            : "+v"(ep.bits), "=&v"(t)
+            : "v"(w), "s"(k_pair1));
     };
     // (inline asm so that the IR passes cannot sink the packing to its use after the GEMM: it is
     //  meant to run in the MFMA gap where the hook places it; v_cvt_pk_bf16_f32 rounds to nearest
@@ -546,10 +554,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                     : "v"(ep.vp), "v"(ep.xo));
                 ep.hw[e >> 1] = w;
                 ep.lw[e >> 1] = wl;
+                mask_pair(w);
             } else {
                 uint32_t w;
                 asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(ep.vp), "v"(ep.xo));
                 ep.hw[e >> 1] = w;
+                mask_pair(w);
             }
         }
     };
@@ -573,6 +583,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         ep.hw[e >> 1] = w;
         ep.ta = t0;
         ep.tb = t1;
+        mask_pair(w);
     };
     auto fpackB = [&](auto ec) {
         constexpr int e = decltype(ec)::value;
@@ -606,7 +617,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             Ol[2 * rt].u = make_uint4(ep.lw[0], ep.lw[1], ep.lw[2], ep.lw[3]);
             Ol[2 * rt + 1].u = make_uint4(ep.lw[4], ep.lw[5], ep.lw[6], ep.lw[7]);
         }
-        if constexpr ((rt & 1) == 0) mpend = ep.bits << 16;
+        if constexpr ((rt & 1) == 0) mpend = ep.bits << 8;
         else mks[(l * C::NMW + (rt >> 1)) * 64 + lane] = mpend | ep.bits;
         if (save) store_rt(srow, rtc, Oh[2 * rt], Oh[2 * rt + 1]);
     };
@@ -617,7 +628,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         return;
 #endif
         constexpr int rt = decltype(rtc)::value;
-        constexpr int bit = 16 * (1 - (rt & 1)) + 15 - e;
+        // (mask_pair's layout: pair e >> 1, odd elements in the upper stream, even row tiles << 8)
+        constexpr int bit = 16 * (e & 1) + 8 * (1 - (rt & 1)) + 7 - (e >> 1);
         float x;
         asm volatile(  // x = relu'(z) ? acc : 0 from the mask bit (in the gap, as fpack)
             "v_bfe_i32 %0, %1, %3, 1\n\t"
@@ -764,7 +776,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         // layer 0: r0 row tiles share a stage (their few k-steps fill one slot)
                         const int sub = l == 0 ? rt % a.r0 : 0;
                         // the bias (a static LDS table) before the stage wait: its reads overlap it
+                        S2T_BEGIN(15);
                         cur = bias_init(boff, rt);
+                        S2T_END(15);
                         if (sub == 0) slot0 = stage_begin(l == 0);  // layer 0: the pieces in a burst
                         const char* slot = slot0 + sub * a.nk0 * 1024;
                         // the next tile's target / mask / H into the other input buffer (the tile that
@@ -799,28 +813,34 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                                 }
                             }, PcL());
                             S2T_END(8);
+                            S2T_BEGIN(13);
                             if constexpr (SPLITPK) fpackB(std::integral_constant<int, 15>());
                             s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
                                 if (decltype(ec)::value >= MS * nk) fstep(prv, ec);
                             });
+                            S2T_END(13);
                             S2T_BEGIN(10);
                             ffinish(l, std::integral_constant<int, rt - 1>(), save, srow, mks);
                             S2T_END(10);
                         }
                         if (rt == nrt - 1) {
+                            S2T_BEGIN(13);
                             ep.bits = 0;
                             s2_sfor<16>([&](auto ec) { fstep(cur, ec); });
                             ffinish(l, rtc, save, srow, mks);
+                            S2T_END(13);
                         }
                     } else {
                         zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
                     }
                 });
+                S2T_BEGIN(14);
 #pragma unroll
                 for (int k = 0; k < NKH; ++k) {
                     Bh[k] = Oh[k];
                     if constexpr (SPLIT) Bl[k] = Ol[k];
                 }
+                S2T_END(14);
             };
             fwd_layer(0, F0h, F0l, a.nk0, NK0t(), std::integral_constant<int, 2>());
             for (int l = 1; l < nl - 1; ++l) fwd_layer(l, Bh, Bl, NKH, NKHt(), std::integral_constant<int, 1>());

@@ -91,8 +91,12 @@ def _ensure_current():
     if have == want:
         return
     if not default:
-        raise RuntimeError(f"libmarf: {LIB_PATH} was built from other sources (hash {have}, sources {want}); "
-                           "rebuild it (build_lib.py --variant)")
+        # an explicitly chosen library (MARF_LIB: A/B and diagnostic builds, possibly of other
+        # sources on purpose) is loaded, but never silently
+        import sys
+        print(f"[marf] warning: MARF_LIB={LIB_PATH} was built from other sources (hash {have}, tree {want})",
+              file=sys.stderr, flush=True)
+        return
     try:
         build_lib.build(force=True, verbose=False)
     except Exception as e:  # pragma: no cover - message path
@@ -101,7 +105,7 @@ def _ensure_current():
 
 def lib():
     """Load libmarf.so; a library built from other sources than the ones in this tree is rebuilt
-    (default path) or refused (MARF_LIB variants), never loaded silently."""
+    (default path) or loaded with a warning (an explicit MARF_LIB), never loaded silently."""
     global _lib
     if _lib is None:
         _ensure_current()

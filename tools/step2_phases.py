@@ -17,7 +17,8 @@ import bench  # noqa: E402
 NAMES = ["stage wait+barrier", "DMA issue", "backward (BWL..BW0)", "dH tail", "prologue", "forward (FW0..FWH)",
          "last layer + dW_last", "tile loop total", "  in fwd GEMM bodies", "  in dgrad GEMM bodies",
          "  fwd tile finish (frag regs, mask, stores)", "  dgrad tile finish (frag regs, stores)",
-         "  stage vmcnt/lgkmcnt wait (of wait+barrier)"]
+         "  stage vmcnt/lgkmcnt wait (of wait+barrier)", "  fwd epilogue steps outside GEMM bodies",
+         "  fwd operand copies (B = O)", "  fwd bias init"]
 
 
 def main():
@@ -45,7 +46,7 @@ def main():
         v = m.graph.forward(var)
         m.graph.compute_loss(v).rgb.backward()
     torch.cuda.synchronize()
-    st = stamps.view(-1, 16).cpu().numpy().astype(np.float64)[:, :13]
+    st = stamps.view(-1, 16).cpu().numpy().astype(np.float64)[:, :16]
     st = st[st[:, 7] > 0]
     tiles = 4194304 // (32 * (4 if args.precision == "bf16x3" else 8)) / len(st)
     mean = st.mean(0) / tiles
