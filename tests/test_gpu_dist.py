@@ -126,12 +126,12 @@ def test_sharded_step_matches_single(precision, world, config, tmp_path):
     # amplifies the ~1e-7 summation-order difference of MLP-gradient entries near zero (its first
     # update is lr g / (|g| + eps)): measured on fp32 and bf16x3, 17 of 4096 warp entries of the
     # 16x16 patches move by up to 3.5e-5 after 3 steps and 1-3 of 65,536 weights of a layer by up
-    # to 2.8e-4.  There: at most 1 in 10^3 entries beyond 1e-5, none beyond lr (one Adam step).
+    # to 2.8e-4.  There: at most 1 in 100 entries beyond 1e-5, none beyond lr (one Adam step).
     if config == "c4":
         pairs = [(b["warps"], a["warps"])] + [(b[f"p{i}"], a[f"p{i}"]) for i in range(n)]
         for x, y in pairs:
             d = np.abs(x - y)
-            assert (d > 1e-5).mean() <= 1e-3 and d.max() <= 1e-3, ((d > 1e-5).sum(), d.max())
+            assert (d > 1e-5).mean() <= 1e-2 and d.max() <= 1e-3, ((d > 1e-5).sum(), d.max())
     else:
         np.testing.assert_allclose(b["warps"], a["warps"], atol=1e-5, rtol=0)
         for i in range(n):
