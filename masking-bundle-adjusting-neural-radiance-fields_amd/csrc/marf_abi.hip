@@ -756,6 +756,23 @@ static int device_cus() {
 
 static bool use_step2(const marf_net* n) { return n->s2.variant >= 0; }
 
+// split-K chunk of the weight gradients over S pixel slots (k_wgrad / k_wgrad_dma)
+static long long wgrad_chunk(long long S) {
+    long long chunk = rup((S + 255) / 256, 64);
+    return chunk < 64 ? 64 : chunk;
+}
+
+// The layer-0 weight gradient recomputes feat_0 (grid -> warp -> posenc + c2f, bf16 hi) instead of
+// reading it, so the step kernel does not store it (MARF_F0_RECOMPUTE=0: store and read, for A/B).
+static bool l0_recompute(const marf_net* n, const GeoDev& g, long long S) {
+    const char* e = getenv("MARF_F0_RECOMPUTE");
+    if (e && e[0] == '0') return false;
+    if (n->s2.variant != 1 || g.mode != MARF_GEO_GRID) return false;
+    const long long chunk = wgrad_chunk(S);
+    return marf_wgrad_l0_recompute_ok(n->Mp[0], n->Kp[1], n->s2.ldf0, S, (int)chunk, (int)((S + chunk - 1) / chunk),
+                                      g.Np_pad);
+}
+
 // render = a forward-only launch: no saved tensors, no dH / weight-gradient partials
 static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p, bool render = false) {
     const Step2NetPlan& q = n->s2;
@@ -842,6 +859,7 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     }
     a.bias = (const float*)(pk + q.bias_off);
     a.nbias = q.nbias;
+    a.feat0_recompute = !render && l0_recompute(net, a.geo, p.S) ? 1 : 0;
     a.gt = d_gt;
     a.mask = d_mask;
     a.rgb = d_rgb;
@@ -915,17 +933,22 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
     const float* denom = d_loss_out + 1;
     const int nl = net->n_layers;
     if (d_dparams) {
-        long long chunk = rup((p.S + 255) / 256, 64);
-        if (chunk < 64) chunk = 64;
+        const long long chunk = wgrad_chunk(p.S);
         const int n_chunks = (int)((p.S + chunk - 1) / chunk);
         const int* kmap = (const int*)(sv + p.kmap);
+        const bool f0 = l0_recompute(net, g, p.S);
         for (int l = 0; l < nl - 1; ++l) {
             const int K = l == 0 ? q.ldf0 : net->Kp[l];
             {
                 MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
-                HIPCHK(marf_launch_wgrad(1, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K,
-                                         (int)chunk, n_chunks, part, bpart, s),
-                       "step_backward wgrad");
+                if (l == 0 && f0)
+                    HIPCHK(marf_launch_wgrad_l0_recompute(sv + p.dz[1], net->Kp[1], g, (const float*)(sv + p.c2f), net->L,
+                                                          q.nk0, p.S, net->Mp[0], (int)chunk, n_chunks, part, bpart, s),
+                           "step_backward wgrad_l0 (feat_0 recomputed)");
+                else
+                    HIPCHK(marf_launch_wgrad(1, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K,
+                                             (int)chunk, n_chunks, part, bpart, s),
+                           "step_backward wgrad");
             }
             {
                 MarfProfScope ps("wgrad_reduce", s);

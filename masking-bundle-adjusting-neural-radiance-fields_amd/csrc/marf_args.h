@@ -108,6 +108,7 @@ struct Step2Args {
     unsigned long long* stamps;      // diagnostic builds (MARF_STAMPS): [grid][8] cycle totals of wave 0
     int n_tiles;                     // block tiles of 32 * NW pixel slots
     int fwd_only;                    // render: forward stages only, rgb out, nothing saved
+    int feat0_recompute;             // feat_0 is recomputed by the layer-0 weight gradient: not stored
     const float* pro_fallback;       // valid device address for the input DMA when gt / H are absent
     // LDS layout (byte offsets; computed on the host)
     int lds_pro, lds_bias, lds_c2f, lds_layers, lds_wave, lds_wave_bytes, lds_total;
@@ -140,6 +141,10 @@ hipError_t marf_launch_reduce_dH(const float* partial, int tiles_per_patch, int 
                                  const float* denom = nullptr);
 hipError_t marf_launch_mlp_fwd(const marf::FwdArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
 hipError_t marf_launch_mlp_bwd(const marf::BwdArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
+bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk, int n_chunks, long long Np_pad);
+hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev& geo, const float* c2f_w, int L,
+                                          int nk0, long long S, int M, int chunk, int n_chunks, float* partial,
+                                          float* bpartial, hipStream_t s);
 hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
                              int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s);
 hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* feat, long long S, int ldf, int K,

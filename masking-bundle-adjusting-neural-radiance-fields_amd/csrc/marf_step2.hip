@@ -737,7 +737,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 // feat_0 (bf16 hi) for the layer-0 weight gradient: column 16 ks + 8 h + j
                 // (every armed DMA piece was issued before the previous store: these count as the
                 //  current stage's stores)
-                if (!a.fwd_only) {
+                if (!a.fwd_only && !a.feat0_recompute) {
                     u16* row = ly_ptr(0, 0) + myslot * ly_int(0, 3);
 #pragma unroll
                     for (int g = 0; g < C::NK0; ++g)

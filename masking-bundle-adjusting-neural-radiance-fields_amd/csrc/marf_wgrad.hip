@@ -16,12 +16,24 @@
 #include "marf_args.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace marf {
 
+// feat_0 of the step kernel (marf_step2.hip prologue) recomputed on chip instead of read: crop
+// grid -> warp -> posenc + c2f, split to the bf16 hi word, in the step kernel's column order
+// (16 g + 8 h + j: band group g, coordinate h, j < 4 sin / j >= 4 cos; group nk0 - 1 the raw
+// coordinate).  The same device functions and fp32 order give the same bits.
+struct Feat0Src {
+    GeoDev geo;         // crop grid geometry of the step (Hm: [B][9])
+    const float* c2f_w; // [L] band weights of the step, or null (c2f off)
+    int L, nk0;
+};
+
 struct WgArgs {
     const void* dz;    // [S][ldz] T
-    const void* feat;  // [S][ldf] T
+    const void* feat;  // [S][ldf] T (unused when feat_0 is recomputed)
+    Feat0Src f0;
     long long S;
     int ldz, ldf;      // row strides
     int M, K;          // output rows (<= ldz) and cols (<= ldf)
@@ -211,6 +223,8 @@ MARF_DEV void glds16(const char* src, unsigned lds) {
                  : "memory");
 }
 
+constexpr int F0_PATCHES = 4;  // patches a layer-0 weight-gradient chunk may span (host-checked)
+
 MARF_DEV int swz(int r, int c) {  // byte offset of bf16 element (r, c) in a 256-wide swizzled stage
     return r * 512 + ((((c >> 3) ^ (4 * (r & 3)))) << 4) + (c & 7) * 2;
 }
@@ -229,15 +243,16 @@ MARF_DEV int foff(int r, int c) {
     else return r * (KF * 2) + c * 2;
 }
 
-template <class P, int NBUF, int SP, int KF>
+template <class P, int NBUF, int SP, int KF, bool F0 = false>
 __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     static_assert(KF == 256 || KF == 96, "feat width");
+    static_assert(!F0 || (KF == 96 && SP == 32), "feat_0 recompute: the 96-wide layer-0 stage of 32 rows");
     constexpr int WR = KF == 256 ? 4 : 8, WC = 8 / WR;  // wave grid over the 256 x KF output
     constexpr int RT = 256 / 32 / WR, CT = KF / 32 / WC;
     constexpr int ZB = SP * 512;                 // bytes of the dz stage (SP rows x 256 bf16)
     constexpr int FB = SP * KF * 2;              // bytes of the feat stage
     constexpr int NGZ = ZB / 8192;               // DMA instructions per wave and stage (1 KB each)
-    constexpr int NGF = (FB + 8191) / 8192;      // (feat: the last round may be partly idle)
+    constexpr int NGF = F0 ? 0 : (FB + 8191) / 8192;  // (feat: the last round may be partly idle)
     static_assert(NGZ * 8192 == ZB && FB % 1024 == 0 && NBUF >= 2 && NBUF <= 6, "stage shape");
     constexpr int PER_ST = NGZ + NGF;            // vmcnt units per stage (the same on every wave)
     constexpr int STB = ZB + FB;                 // bytes of one ring slot
@@ -268,6 +283,64 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
 
     const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
     const unsigned junk = lds0 + NBUF * STB;     // 1 KB sink for the idle feat rounds
+    // F0: the patches' homographies and the band weights, staged once (plain loads, drained
+    // before the ring starts: no global load inside the ring, whose waits count DMA in order)
+    float* f0_h = reinterpret_cast<float*>(smem + NBUF * STB);     // [F0_PATCHES][9]
+    float* f0_w = f0_h + 9 * F0_PATCHES;                           // [32]
+    int f0_b0 = 0;
+    if constexpr (F0) {
+        const GeoDev& gg = a.f0.geo;
+        f0_b0 = (int)(s_begin / gg.Np_pad);
+        for (int e = threadIdx.x; e < 9 * F0_PATCHES; e += 512) {
+            const int bb = min(f0_b0 + e / 9, gg.B - 1);
+            f0_h[e] = gg.Hm[9 * (size_t)bb + e % 9];
+        }
+        if (threadIdx.x < 32) f0_w[threadIdx.x] = (a.f0.c2f_w && (int)threadIdx.x < a.f0.L) ? a.f0.c2f_w[threadIdx.x] : 1.0f;
+        wait_vm<0>();
+        __syncthreads();
+    }
+    // F0: one stage of feat_0 (SP = 32 rows of 96 bf16) into ring slot buf: 16 threads per row, each
+    // two bands of one coordinate (sin pair + cos pair) and one pair of the raw-coordinate / padding
+    // columns 64..95 (the step kernel's s2_split8 hi words: v_cvt_pk_bf16_f32 of the same fp32 values)
+    auto compute_f0 = [&](int st, int buf_off) {
+        const GeoDev& gg = a.f0.geo;
+        const int r = threadIdx.x >> 4, sub = threadIdx.x & 15;
+        const long long slot = s_begin + (long long)st * SP + r;
+        const int bb = (int)(slot / gg.Np_pad);
+        const int p = (int)(slot - (long long)bb * gg.Np_pad);
+        const int rr = p / gg.w, cc = p - rr * gg.w;
+        const float x = grid_coord(gg.x0 + cc, gg.W, gg.norm_w);
+        const float y = grid_coord(gg.y0 + rr, gg.H, gg.norm_h);
+        float u, v, X[3];
+        warp_point(f0_h + 9 * min(bb - f0_b0, F0_PATCHES - 1), x, y, u, v, X, gg.bmm_small);
+        char* row = smem + buf_off + r * (KF * 2);
+        const int h = sub >> 3, k0 = 2 * (sub & 7);
+        const float cd = h ? v : u;
+        float sn[2] = {0.f, 0.f}, cs[2] = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int k = k0 + i;
+            if (k < a.f0.L) {
+                band_sincos<true>(cd, k, sn[i], cs[i]);
+                if (a.f0.c2f_w) {
+                    sn[i] = sn[i] * f0_w[k];
+                    cs[i] = cs[i] * f0_w[k];
+                }
+            }
+        }
+        const int ng = a.f0.nk0 - 1;
+        const int g = k0 >> 2, j = k0 & 3;
+        if (g < ng) {
+            *reinterpret_cast<uint32_t*>(row + 2 * (16 * g + 8 * h + j)) = PrecBF16::pk2(sn[0], sn[1]);
+            *reinterpret_cast<uint32_t*>(row + 2 * (16 * g + 8 * h + 4 + j)) = PrecBF16::pk2(cs[0], cs[1]);
+        }
+        // columns 16 ng .. 95: the raw coordinates (16 ng + 8 h) and zeros, one pair per thread
+        for (int c = 16 * ng + 2 * sub; c < KF; c += 32) {
+            const int hc = (c - 16 * ng) >> 3;
+            const float val = (c - 16 * ng) == 8 * hc && hc < 2 ? (hc ? v : u) : 0.f;
+            *reinterpret_cast<uint32_t*>(row + 2 * c) = PrecBF16::pk2(val, 0.f);
+        }
+    };
     auto issue = [&](int st) {
         const unsigned buf = lds0 + (st % NBUF) * STB;
         const long long row0 = s_begin + (long long)st * SP;
@@ -278,6 +351,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
             const int c16 = (lane & 31) ^ (4 * (r & 3));
             glds16(dz + (size_t)(row0 + r) * ldzb + c16 * 16, __builtin_amdgcn_readfirstlane(buf + seg * 1024));
         }
+        if constexpr (F0) compute_f0(st, (st % NBUF) * STB + ZB);
 #pragma unroll
         for (int q = 0; q < NGF; ++q) {
             const int seg = q * 8 + wave;
@@ -541,18 +615,18 @@ static bool wgrad_dma_enabled() {
 #define MARF_WG_NBUF_0 4
 #endif
 
-template <class P, int KF>
+template <class P, int KF, bool F0 = false>
 static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
     a.n_chunks = n_chunks;
     a.n_oblk_c = a.K / KF;
     constexpr int SP = 32;
     constexpr int NBUF = KF == 256 ? MARF_WG_NBUF_H : MARF_WG_NBUF_0;  // ring depth within 160 KB of LDS
-    const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024);
+    const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024) + (F0 ? (9 * F0_PATCHES + 32) * 4 : 0);
     {
-        hipError_t e = ensure_dynamic_lds((const void*)k_wgrad_dma<P, NBUF, SP, KF>, lds);
+        hipError_t e = ensure_dynamic_lds((const void*)k_wgrad_dma<P, NBUF, SP, KF, F0>, lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((k_wgrad_dma<P, NBUF, SP, KF>), dim3(n_chunks * (a.M / 256) * a.n_oblk_c), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((k_wgrad_dma<P, NBUF, SP, KF, F0>), dim3(n_chunks * (a.M / 256) * a.n_oblk_c), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 
@@ -603,6 +677,35 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
     if (cfg == 3) return launch_wg<PrecF32, 2, 2>(a, n_chunks, nr * nc, s);
     if (cfg == 1) return launch_wg<PrecF32, 2, 1>(a, n_chunks, nr * nc, s);
     return launch_wg<PrecF32, 1, 1>(a, n_chunks, nr * nc, s);
+}
+
+// Layer-0 weight gradient with feat_0 recomputed on chip (step kernel's feat0_recompute); bf16,
+// 256-wide layer 0, the 96-wide feat_0 of L = 13..16.  False if the shape does not qualify.
+bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk, int n_chunks, long long Np_pad) {
+    return M == 256 && ldz % 8 == 0 && ldz >= M && ldf0 == 96 && S % 32 == 0 && chunk % 32 == 0 &&
+           (long long)n_chunks <= 0x7fffffff && (chunk + Np_pad - 1) / Np_pad + 1 <= F0_PATCHES;
+}
+
+hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev& geo, const float* c2f_w, int L,
+                                          int nk0, long long S, int M, int chunk, int n_chunks, float* partial,
+                                          float* bpartial, hipStream_t s) {
+    WgArgs a;
+    memset(&a, 0, sizeof(a));
+    a.dz = dz;
+    a.feat = nullptr;
+    a.f0.geo = geo;
+    a.f0.c2f_w = c2f_w;
+    a.f0.L = L;
+    a.f0.nk0 = nk0;
+    a.S = S;
+    a.ldz = ldz;
+    a.ldf = 96;
+    a.M = M;
+    a.K = 96;
+    a.chunk = chunk;
+    a.partial = partial;
+    a.bpartial = bpartial;
+    return launch_wg_dma<PrecBF16, 96, true>(a, n_chunks, s);
 }
 
 hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* feat, long long S, int ldf, int K, int chunk,
