@@ -7,6 +7,8 @@
 // pixel per lane and features in registers.  256 threads = 4 waves; output row tiles (32) of a
 // layer are dealt round-robin to the 4 waves, each wave covers all PT = TP/32 pixel tiles.
 #pragma once
+#include <type_traits>
+
 #include "marf_args.h"
 
 namespace marf {
@@ -102,8 +104,11 @@ struct TileStore {
 // reloaded for k-step k+4 right after its MFMAs issue: three k-steps of latency cover, no register
 // moves), the activation fragments of step k+1 are read from LDS while step k's MFMAs run (two
 // statically named buffers).  Loads past the last k-step are clamped to it (harmless L2 hits).
-// JOB: one TileStore chunk per k-step (read before the B prefetch, stored after the A reload).
-template <class P, int NA, int RT, int PT, bool JOB, int NW = 4>
+// JOB: one TileStore chunk per k-step (1) or per second k-step (2: the job has at most half as many
+// chunks as the GEMM k-steps, e.g. a 512-wide tile saved during a 512-deep GEMM at 8 waves, where
+// one chunk per k-step would rewrite the last chunk for half the GEMM), read before the B
+// prefetch, stored after the A reload.
+template <class P, int NA, int RT, int PT, int JOB, int NW = 4>
 MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__ W, int K,
                         const typename P::T* act, int lda, int wave, int lane, TileStore<typename P::T>& st) {
     typedef typename P::frag F;
@@ -132,12 +137,18 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
             for (int i = 0; i < NA; ++i) acc[i][j] = P::mma32(a[i], b[j], acc[i][j]);
     };
     uint4 sv = make_uint4(0, 0, 0, 0);
-    auto sread = [&]() {
-        if constexpr (JOB) sv = st.read(act);
+    // pos: the k-step's position in the 4-step unrolled body (0 in the 2-deep-ring body, which
+    // places the job at positions 0 and 1 of its 2-step iterations)
+    auto sread = [&](auto posc) {
+        if constexpr (JOB == 1 || (JOB == 2 && decltype(posc)::value % 2 == 0)) sv = st.read(act);
     };
-    auto swrite = [&]() {
-        if constexpr (JOB) st.write(sv);
+    auto swrite = [&](auto posc) {
+        if constexpr (JOB == 1 || (JOB == 2 && decltype(posc)::value % 2 == 0)) st.write(sv);
     };
+    typedef std::integral_constant<int, 0> J0;
+    typedef std::integral_constant<int, 1> J1;
+    typedef std::integral_constant<int, 2> J2;
+    typedef std::integral_constant<int, 3> J3;
     F A0[NA], A1[NA], A2[NA], A3[NA], B0[PT], B1[PT];
     if constexpr (sizeof(F) * NA > 32) {
         // wide row blocks (bf16, NA > 2): a 2-deep ring keeps the kernel inside 256 VGPRs
@@ -146,20 +157,20 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
         ldB(B0, 0);
         int k = 0;
         for (; k + 2 <= nk; k += 2) {
-            sread();
+            sread(J0());
             ldB(B1, k + 1);
             __builtin_amdgcn_sched_barrier(0);
             mma(A0, B0);
             __builtin_amdgcn_sched_barrier(0);
             ldA(A0, k + 2);
-            swrite();
-            sread();
+            swrite(J0());
+            sread(J1());
             ldB(B0, k + 2);
             __builtin_amdgcn_sched_barrier(0);
             mma(A1, B1);
             __builtin_amdgcn_sched_barrier(0);
             ldA(A1, k + 3);
-            swrite();
+            swrite(J1());
         }
         if (k < nk) mma(A0, B0);
         if constexpr (JOB) st.flush(act);
@@ -174,34 +185,34 @@ MARF_DEV void gemm_rows(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
     // sched_barrier pins the issue order: left alone, the scheduler sinks every weight load to
     // the loop end (one MFMA of latency cover) and folds the two B buffers into one.
     for (; k + 4 <= nk; k += 4) {
-        sread();
+        sread(J0());
         ldB(B1, k + 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(A0, B0);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A0, k + 4);
-        swrite();
-        sread();
+        swrite(J0());
+        sread(J1());
         ldB(B0, k + 2);
         __builtin_amdgcn_sched_barrier(0);
         mma(A1, B1);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A1, k + 5);
-        swrite();
-        sread();
+        swrite(J1());
+        sread(J2());
         ldB(B1, k + 3);
         __builtin_amdgcn_sched_barrier(0);
         mma(A2, B0);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A2, k + 6);
-        swrite();
-        sread();
+        swrite(J2());
+        sread(J3());
         ldB(B0, k + 4);
         __builtin_amdgcn_sched_barrier(0);
         mma(A3, B1);
         __builtin_amdgcn_sched_barrier(0);
         ldA(A3, k + 7);
-        swrite();
+        swrite(J3());
     }
     // remainder (nk % 4 steps): A0..A2 hold steps k..k+2, B0 holds step k
     if (k < nk) {
@@ -242,20 +253,30 @@ MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
     }
     int na = (n_rt - wave + NW - 1) / NW;
     na = na < 0 ? 0 : (na > RT ? RT : na);
-    if (st.active) {
+    // the job's chunks at every k-step, or at every second one when that still covers them
+    const bool half = st.active && 2 * st.nq <= K / P::KS;
+    if (st.active && half) {
         switch (na) {
-            case 1: gemm_rows<P, 1, RT, PT, true, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 2: gemm_rows<P, 2, RT, PT, true, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, true, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, true, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 1: gemm_rows<P, 1, RT, PT, 2, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 2: gemm_rows<P, 2, RT, PT, 2, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, 2, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, 2, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            default: st.flush(act); break;
+        }
+    } else if (st.active) {
+        switch (na) {
+            case 1: gemm_rows<P, 1, RT, PT, 1, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 2: gemm_rows<P, 2, RT, PT, 1, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, 1, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, 1, NW>(acc, W, K, act, lda, wave, lane, st); break;
             default: st.flush(act); break;
         }
     } else {
         switch (na) {
-            case 1: gemm_rows<P, 1, RT, PT, false, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 2: gemm_rows<P, 2, RT, PT, false, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, false, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, false, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 1: gemm_rows<P, 1, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 2: gemm_rows<P, 2, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
+            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
             default: break;
         }
     }

@@ -287,6 +287,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     // before the ring starts: no global load inside the ring, whose waits count DMA in order)
     float* f0_h = reinterpret_cast<float*>(smem + NBUF * STB);     // [F0_PATCHES][9]
     float* f0_w = f0_h + 9 * F0_PATCHES;                           // [32]
+    float* f0_uv = f0_w + 32;                                      // [NBUF + 1][SP][2] warped coordinates
     int f0_b0 = 0;
     if constexpr (F0) {
         const GeoDev& gg = a.f0.geo;
@@ -299,12 +300,11 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         wait_vm<0>();
         __syncthreads();
     }
-    // F0: one stage of feat_0 (SP = 32 rows of 96 bf16) into ring slot buf: 16 threads per row, each
-    // two bands of one coordinate (sin pair + cos pair) and one pair of the raw-coordinate / padding
-    // columns 64..95 (the step kernel's s2_split8 hi words: v_cvt_pk_bf16_f32 of the same fp32 values)
-    auto compute_f0 = [&](int st, int buf_off) {
+    // F0: the warped coordinates of a stage's SP rows (one thread per row) into uv slot
+    // st % (NBUF + 1): stages 0..NBUF-1 before the ring starts, stage st + NBUF in main iteration st
+    // (the slot of stage st - 1, whose feat_0 was built before an earlier barrier)
+    auto warp_rows = [&](int st, int r) {
         const GeoDev& gg = a.f0.geo;
-        const int r = threadIdx.x >> 4, sub = threadIdx.x & 15;
         const long long slot = s_begin + (long long)st * SP + r;
         const int bb = (int)(slot / gg.Np_pad);
         const int p = (int)(slot - (long long)bb * gg.Np_pad);
@@ -313,6 +313,20 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         const float y = grid_coord(gg.y0 + rr, gg.H, gg.norm_h);
         float u, v, X[3];
         warp_point(f0_h + 9 * min(bb - f0_b0, F0_PATCHES - 1), x, y, u, v, X, gg.bmm_small);
+        f0_uv[((st % (NBUF + 1)) * SP + r) * 2] = u;
+        f0_uv[((st % (NBUF + 1)) * SP + r) * 2 + 1] = v;
+    };
+    if constexpr (F0) {
+        if ((int)threadIdx.x < SP * NBUF && (int)threadIdx.x / SP < n_st) warp_rows(threadIdx.x / SP, threadIdx.x % SP);
+        __syncthreads();
+    }
+    // F0: one stage of feat_0 (SP = 32 rows of 96 bf16) into its ring slot: 16 threads per row, each
+    // two bands of one coordinate (sin pair + cos pair) and one pair of the raw-coordinate / padding
+    // columns 64..95 (the step kernel's s2_split8 hi words: v_cvt_pk_bf16_f32 of the same fp32 values).
+    // Stage st's coordinates were warped before a barrier that precedes this call.
+    auto compute_f0 = [&](int st, int buf_off) {
+        const int r = threadIdx.x >> 4, sub = threadIdx.x & 15;
+        const float u = f0_uv[((st % (NBUF + 1)) * SP + r) * 2], v = f0_uv[((st % (NBUF + 1)) * SP + r) * 2 + 1];
         char* row = smem + buf_off + r * (KF * 2);
         const int h = sub >> 3, k0 = 2 * (sub & 7);
         const float cd = h ? v : u;
@@ -388,6 +402,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         // every wave is past its reads of buffer (st - 1) % NBUF: refill it
+        if constexpr (F0) {
+            if ((int)threadIdx.x < SP && st + NBUF < n_st) warp_rows(st + NBUF, threadIdx.x);
+        }
         if (st + NBUF - 1 < n_st) issue(st + NBUF - 1);
 
         const char* tz = smem + (st % NBUF) * STB;
@@ -621,7 +638,7 @@ static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
     a.n_oblk_c = a.K / KF;
     constexpr int SP = 32;
     constexpr int NBUF = KF == 256 ? MARF_WG_NBUF_H : MARF_WG_NBUF_0;  // ring depth within 160 KB of LDS
-    const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024) + (F0 ? (9 * F0_PATCHES + 32) * 4 : 0);
+    const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024) + (F0 ? (9 * F0_PATCHES + 32 + (NBUF + 1) * SP * 2) * 4 : 0);
     {
         hipError_t e = ensure_dynamic_lds((const void*)k_wgrad_dma<P, NBUF, SP, KF, F0>, lds);
         if (e != hipSuccess) return e;
