@@ -402,8 +402,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         // every wave is past its reads of buffer (st - 1) % NBUF: refill it
-        if constexpr (F0) {
-            if ((int)threadIdx.x < SP && st + NBUF < n_st) warp_rows(st + NBUF, threadIdx.x);
+        if constexpr (F0) {  // rows spread over the 8 waves (lanes 0-3 of each): no wave carries them all
+            if (lane < SP / 8 && st + NBUF < n_st) warp_rows(st + NBUF, wave * (SP / 8) + lane);
         }
         if (st + NBUF - 1 < n_st) issue(st + NBUF - 1);
 
