@@ -365,7 +365,6 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
             const int c16 = (lane & 31) ^ (4 * (r & 3));
             glds16(dz + (size_t)(row0 + r) * ldzb + c16 * 16, __builtin_amdgcn_readfirstlane(buf + seg * 1024));
         }
-        if constexpr (F0) compute_f0(st, (st % NBUF) * STB + ZB);
 #pragma unroll
         for (int q = 0; q < NGF; ++q) {
             const int seg = q * 8 + wave;
@@ -380,6 +379,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
                 glds16(src, __builtin_amdgcn_readfirstlane(real ? buf + ZB + seg * 1024 : junk));
             }
         }
+        if constexpr (F0) compute_f0(st, (st % NBUF) * STB + ZB);  // after the stage's DMA is in flight
     };
 
     f32x16 acc[RT][CT];
@@ -402,10 +402,10 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         // every wave is past its reads of buffer (st - 1) % NBUF: refill it
-        if constexpr (F0) {  // rows spread over the 8 waves (lanes 0-3 of each): no wave carries them all
-            if (lane < SP / 8 && st + NBUF < n_st) warp_rows(st + NBUF, wave * (SP / 8) + lane);
-        }
         if (st + NBUF - 1 < n_st) issue(st + NBUF - 1);
+        if constexpr (F0) {  // the last wave warps the rows of stage st + NBUF (one lane per row)
+            if (wave == 7 && lane < SP && st + NBUF < n_st) warp_rows(st + NBUF, lane);
+        }
 
         const char* tz = smem + (st % NBUF) * STB;
         const char* tf = tz + ZB;
