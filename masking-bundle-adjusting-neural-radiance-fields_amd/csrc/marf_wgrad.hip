@@ -288,10 +288,13 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     float* f0_h = reinterpret_cast<float*>(smem + NBUF * STB);     // [F0_PATCHES][9]
     float* f0_w = f0_h + 9 * F0_PATCHES;                           // [32]
     float* f0_uv = f0_w + 32;                                      // [NBUF + 1][SP][2] warped coordinates
-    int f0_b0 = 0;
+    int f0_b0 = 0, f0_p0 = 0;
+    float f0_inv_w = 0.f;
     if constexpr (F0) {
         const GeoDev& gg = a.f0.geo;
         f0_b0 = (int)(s_begin / gg.Np_pad);
+        f0_p0 = (int)(s_begin - (long long)f0_b0 * gg.Np_pad);
+        f0_inv_w = 1.0f / (float)gg.w;
         for (int e = threadIdx.x; e < 9 * F0_PATCHES; e += 512) {
             const int bb = min(f0_b0 + e / 9, gg.B - 1);
             f0_h[e] = gg.Hm[9 * (size_t)bb + e % 9];
@@ -305,10 +308,17 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     // (the slot of stage st - 1, whose feat_0 was built before an earlier barrier)
     auto warp_rows = [&](int st, int r) {
         const GeoDev& gg = a.f0.geo;
-        const long long slot = s_begin + (long long)st * SP + r;
-        const int bb = (int)(slot / gg.Np_pad);
-        const int p = (int)(slot - (long long)bb * gg.Np_pad);
-        const int rr = p / gg.w, cc = p - rr * gg.w;
+        // division-free: the chunk's first slot split once (f0_b0, f0_p0); a chunk spans at most
+        // F0_PATCHES patches, and p < 2^24 keeps the float quotient within one of the row
+        int p = f0_p0 + st * SP + r, bb = f0_b0;
+        for (int i = 0; i < F0_PATCHES && p >= gg.Np_pad; ++i) {
+            p -= gg.Np_pad;
+            ++bb;
+        }
+        int rr = (int)((float)p * f0_inv_w);
+        rr -= rr * gg.w > p;
+        rr += (rr + 1) * gg.w <= p;
+        const int cc = p - rr * gg.w;
         const float x = grid_coord(gg.x0 + cc, gg.W, gg.norm_w);
         const float y = grid_coord(gg.y0 + rr, gg.H, gg.norm_h);
         float u, v, X[3];
@@ -700,7 +710,7 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
 // 256-wide layer 0, the 96-wide feat_0 of L = 13..16.  False if the shape does not qualify.
 bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk, int n_chunks, long long Np_pad) {
     return M == 256 && ldz % 8 == 0 && ldz >= M && ldf0 == 96 && S % 32 == 0 && chunk % 32 == 0 &&
-           (long long)n_chunks <= 0x7fffffff && (chunk + Np_pad - 1) / Np_pad + 1 <= F0_PATCHES;
+           (long long)n_chunks <= 0x7fffffff && Np_pad < (1 << 24) && (chunk + Np_pad - 1) / Np_pad + 1 <= F0_PATCHES;
 }
 
 hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev& geo, const float* c2f_w, int L,
