@@ -329,15 +329,21 @@ def main():
     peak = PEAK_FP32 if args.precision == "fp32" else PEAK_BF16
     roof = None
     if dom in kflops:
-        avg_s = prof[dom][0] / prof[dom][1] / 1e3
+        # per step: a pipelined step (marf_net_set_pipeline) runs the step kernel in several
+        # launches (pieces of the tiles); FLOPs and bytes are the step's, the time their sum
+        avg_s = prof[dom][0] / args.steps / 1e3
         alg, issued = kflops[dom]
         alg_bytes = 28 * px_local if dom == "mlp_step" else None
         design = step_kernel_bytes(S, Kp0, hidden, 2 if args.precision != "fp32" else 4).get(dom)
         tr = pmc_traffic(args.config, args.precision, dom)
         roof = {"bound": "mfma", "achieved": alg / avg_s / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
                 "frac": alg / avg_s / peak, "traffic": tr[0] if tr else None,
-                "kernel": dom, "avg_launch_ms": avg_s * 1e3, "algorithmic_flops_per_launch": alg,
-                "mfma_flops_per_launch": issued, "mfma_tflops": issued / avg_s / 1e12, "mfma_frac": issued / avg_s / peak,
+                "kernel": dom, "launches_per_step": prof[dom][1] / args.steps,
+                "kernel_ms_per_step": avg_s * 1e3, "avg_launch_ms": prof[dom][0] / prof[dom][1],
+                "algorithmic_flops_per_launch": alg * args.steps / prof[dom][1],
+                "algorithmic_flops_per_step": alg,
+                "mfma_flops_per_launch": issued * args.steps / prof[dom][1], "mfma_flops_per_step": issued,
+                "mfma_tflops": issued / avg_s / 1e12, "mfma_frac": issued / avg_s / peak,
                 "algorithmic_bytes_per_launch": alg_bytes, "design_bytes_per_launch": design,
                 "traffic_ratio": (tr[0] / alg_bytes) if (tr and alg_bytes) else None,
                 "traffic_source": tr[1] if tr else None}

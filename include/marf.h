@@ -114,6 +114,15 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
 void marf_net_destroy(marf_net* net);
 long long marf_net_param_count(const marf_net* net);
 size_t marf_net_packed_bytes(const marf_net* net);
+/* Pipelined weight gradients of the fused step (no reference counterpart: scheduling only; the
+ * reference's loss.all.backward() at model/planar.py:196 computes the same sums).  mode 0 = off
+ * (default; env MARF_PIPE at net creation), 1 = on at any size, -1 = on for large steps.  When on,
+ * marf_step_forward runs the step kernel in pieces of piece_tiles tiles on CUs - wg_blocks blocks
+ * and the split-K weight-gradient partials of each finished piece on wg_blocks CUs of a second
+ * stream; marf_step_backward then only reduces them.  0 = the default size.  Change it between
+ * steps only (the saved-buffer layout of a step depends on it).  Measured slower than the
+ * sequential step on MI355X: off by default. */
+int marf_net_set_pipeline(marf_net* net, int mode, int wg_blocks, int piece_tiles);
 /* fp32 master parameters -> MFMA operand layouts (call after every optimizer step). */
 int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, void* stream);
 

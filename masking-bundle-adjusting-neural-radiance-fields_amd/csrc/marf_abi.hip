@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../../include/marf.h"
@@ -65,6 +66,7 @@ struct marf_net {
     size_t lds_fwd, lds_bwd, lds_step;
     int elem;  // bytes per stored element
     unsigned diag[MARF_MAX_LAYERS];  // numerics-experiment rounding codes (MARF_DIAG_PREC; MARF_DIAG_RT builds)
+    int pipe_mode, pipe_wg, pipe_piece;  // pipelined weight gradients (marf_net_set_pipeline)
 };
 
 // MARF_DIAG_PREC = "WTAD,WTAD,..." per layer (digits: marf_common.h diag_round modes; the last entry
@@ -410,6 +412,14 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
     n->packed_bytes = boff;
     parse_diag(n);
     plan_step2_net(n);
+    {  // defaults of the pipelined weight gradients (marf_net_set_pipeline changes them)
+        const char* e = getenv("MARF_PIPE");
+        n->pipe_mode = e && *e ? atoi(e) : 0;  // off: measured slower
+        e = getenv("MARF_PIPE_WG");
+        n->pipe_wg = e && *e ? atoi(e) : 0;
+        e = getenv("MARF_PIPE_PIECE");
+        n->pipe_piece = e && *e ? atoi(e) : 0;
+    }
     if (n->s2.variant >= 0) n->packed_bytes = n->s2.end_off;
     if (dtype == MARF_BF16X3 && n->s2.variant < 0) {
         delete n;
@@ -421,6 +431,17 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
 }
 
 void marf_net_destroy(marf_net* net) { delete net; }
+
+int marf_net_set_pipeline(marf_net* net, int mode, int wg_blocks, int piece_tiles) {
+    if (!net) return fail(MARF_ERR_INVALID, "net_set_pipeline: NULL net");
+    if (mode < -1 || mode > 1 || wg_blocks < 0 || piece_tiles < 0)
+        return fail(MARF_ERR_INVALID, "net_set_pipeline: mode %d, wg_blocks %d, piece_tiles %d", mode, wg_blocks,
+                    piece_tiles);
+    net->pipe_mode = mode;
+    net->pipe_wg = wg_blocks;
+    net->pipe_piece = piece_tiles;
+    return MARF_OK;
+}
 long long marf_net_param_count(const marf_net* net) { return net ? net->param_count : -1; }
 size_t marf_net_packed_bytes(const marf_net* net) { return net ? net->packed_bytes : 0; }
 
@@ -735,11 +756,24 @@ static void plan_step(const marf_net* n, long long S, StepPlan& p) {
 
 // ---- the pixel-per-wave fused step (marf_step2.hip)
 
+// a pipelined step (plan_pipe, below)
+#define MARF_PIPE_MAXP 64
+struct PipePlan {
+    int on;
+    int G, R, P;    // step-kernel blocks per piece, weight-gradient blocks per piece, pieces
+    int piece;      // tiles per piece (the last one may have fewer)
+    int wg_last;    // weight-gradient blocks of the last piece (every CU)
+    int n_parts;    // split-K partials per layer: (P - 1) R + wg_last
+};
+
 struct Step2BufPlan {
     size_t feat[MARF_MAX_LAYERS], dz[MARF_MAX_LAYERS];
     size_t dH, loss, blast, wlast, dummy, c2f, kmap, part, bpart, total;
+    size_t partl[MARF_MAX_LAYERS], bpartl[MARF_MAX_LAYERS];  // pipelined: per-layer split-K partials
     int grid, n_tiles;
+    int nblk;  // per-block partial sets of the step kernel (all pieces' blocks)
     long long S;
+    PipePlan pipe;
 };
 
 static int device_cus() {
@@ -773,6 +807,82 @@ static bool l0_recompute(const marf_net* n, const GeoDev& g, long long S) {
                                       g.Np_pad);
 }
 
+// ---- pipelined weight gradients (large steps of the pixel-per-wave kernel)
+//
+// The hidden / layer-0 weight gradients re-read the saved feat_l / dz_l: HBM-bound, about a fifth
+// of the step when they follow the whole step kernel.  Their split-K partials do not depend on the
+// upstream gradient (it scales the reduction), so they need not wait for the backward: the step
+// kernel runs in pieces of whole tiles on G = CUs - R blocks (one per CU, persistent), and after
+// each piece the R-block weight-gradient launches of its pixel rows go to a second stream, where
+// they take the R CUs the step kernel leaves free (neither kernel fits beside the other on a CU:
+// LDS), so the re-read of piece j overlaps the step of piece j + 1.  The last piece's weight
+// gradients run on every CU.  Partial (piece j, block b) is j R + b: the reduction order is fixed
+// and the result deterministic (it differs from the one-launch step by fp32 summation order only).
+
+static void plan_pipe(const marf_net* n, const GeoDev& g, long long S, int n_tiles, PipePlan& pp) {
+    memset(&pp, 0, sizeof(pp));
+    const Step2NetPlan& q = n->s2;
+    const int mode = n->pipe_mode;  // 0 off (default), 1 on at any size, -1 large steps only
+    if (mode == 0 || q.variant < 0 || g.mode != MARF_GEO_GRID) return;
+    const int cus = device_cus();
+    int R = n->pipe_wg > 0 ? n->pipe_wg : std::max(1, cus * 7 / 64);  // 28 of 256 CUs
+    R = std::max(1, std::min(R, cus / 2));
+    const int G = cus - R;
+    if (mode < 0 && n_tiles < 16 * cus) return;
+    int piece = n->pipe_piece;
+    if (piece <= 0) {  // about 8 pieces, each a whole number of tile groups per block
+        const int k = std::max(1, (int)std::lround((double)n_tiles / (8.0 * q.NS * G)));
+        piece = k * q.NS * G;
+    }
+    piece = (int)rup(piece, q.NS);
+    int P = (n_tiles + piece - 1) / piece;
+    if (P < 2) {
+        if (mode != 1) return;
+        piece = (int)rup((n_tiles + 1) / 2, q.NS);
+        P = (n_tiles + piece - 1) / piece;
+        if (P < 2) return;
+    }
+    if (P > MARF_PIPE_MAXP) return;
+    // every weight gradient on the range-capable LDS-DMA kernel
+    const int nl = n->n_layers;
+    for (int l = 1; l < nl - 1; ++l)
+        if (!marf_wgrad_range_ok(n->kdt, n->Mp[l], n->Kp[l + 1], n->Kp[l], n->Kp[l])) return;
+    if (!marf_wgrad_range_ok(n->kdt, n->Mp[0], n->Kp[1], q.ldf0, q.ldf0)) return;
+    if (l0_recompute(n, g, S)) {  // the recomputing kernel's ranges may span only a few patches
+        const long long mx = rup((long long)piece * 32 * q.NW / R + 32, 32);
+        if (!marf_wgrad_l0_recompute_ok(n->Mp[0], n->Kp[1], q.ldf0, S, (int)mx, P * cus, g.Np_pad)) return;
+    }
+    pp.on = 1;
+    pp.G = G;
+    pp.R = R;
+    pp.P = P;
+    pp.piece = piece;
+    pp.wg_last = cus;
+    pp.n_parts = (P - 1) * R + cus;
+}
+
+// the second stream and the events of the pipeline, per device (created once)
+struct PipeStreams {
+    hipStream_t s2;
+    hipEvent_t ev[MARF_PIPE_MAXP + 1];
+};
+static int pipe_streams(PipeStreams** out) {
+    static std::mutex mu;
+    static PipeStreams ps[64];
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev), "pipeline: hipGetDevice");
+    if (dev < 0 || dev >= 64) return fail(MARF_ERR_UNSUPPORTED, "pipeline: device %d", dev);
+    std::lock_guard<std::mutex> lk(mu);
+    PipeStreams& p = ps[dev];
+    if (!p.s2) {
+        HIPCHK(hipStreamCreateWithFlags(&p.s2, hipStreamNonBlocking), "pipeline: stream");
+        for (int i = 0; i <= MARF_PIPE_MAXP; ++i)
+            HIPCHK(hipEventCreateWithFlags(&p.ev[i], hipEventDisableTiming), "pipeline: event");
+    }
+    *out = &p;
+    return MARF_OK;
+}
+
 // render = a forward-only launch: no saved tensors, no dH / weight-gradient partials
 static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p, bool render = false) {
     const Step2NetPlan& q = n->s2;
@@ -783,6 +893,10 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
     int cap = device_cus();
     if (const char* e = getenv("MARF_STEP2_GRID")) cap = std::max(1, atoi(e));  // diagnostic override
     p.grid = std::max(1, std::min(p.n_tiles, cap));
+    memset(&p.pipe, 0, sizeof(p.pipe));
+    if (!render) plan_pipe(n, g, p.S, p.n_tiles, p.pipe);
+    if (p.pipe.on) p.grid = p.pipe.G;
+    p.nblk = p.pipe.on ? p.pipe.P * p.pipe.G : p.grid;
     size_t off = 0;
     for (int l = 0; l < nl - 1; ++l) {
         p.feat[l] = off;
@@ -799,11 +913,11 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
     p.dH = off;
     off += rup(Ssave * Ssink / 32 * 9 * 4, 256);
     p.loss = off;
-    off += rup((long long)p.grid * 2 * 8, 256);
+    off += rup((long long)p.nblk * 2 * 8, 256);
     p.blast = off;
-    off += rup((long long)p.grid * 3 * 4, 256);
+    off += rup((long long)p.nblk * 3 * 4, 256);
     p.wlast = off;
-    off += rup((long long)p.grid * 3 * q.Kl * 4, 256);
+    off += rup((long long)p.nblk * 3 * q.Kl * 4, 256);
     p.dummy = off;
     off += rup((long long)p.grid * q.NW * 4 * 64 * 2 * 4, 256);
     p.c2f = off;
@@ -819,11 +933,54 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
         mxo = std::max(mxo, (long long)n->Mp[l] * (l == 0 ? q.ldf0 : n->Kp[l]));
         mxm = std::max(mxm, (long long)n->Mp[l]);
     }
-    p.part = off;
-    off += rup(Ssave * std::max(n_chunks * mxo, 256LL * (3 * q.Kl + 3)) * 4, 256);
-    p.bpart = off;
-    off += rup(Ssave * n_chunks * mxm * 4, 256);
+    if (p.pipe.on) {  // every layer's partials live from the forward to the backward's reduction
+        const long long np = p.pipe.n_parts;
+        for (int l = 0; l < nl - 1; ++l) {
+            p.partl[l] = off;
+            off += rup(np * n->Mp[l] * (l == 0 ? q.ldf0 : n->Kp[l]) * 4, 256);
+            p.bpartl[l] = off;
+            off += rup(np * n->Mp[l] * 4, 256);
+        }
+        p.part = off;  // the fold scratch of the last-layer reduction
+        off += rup(256LL * (3 * q.Kl + 3) * 4, 256);
+        p.bpart = 0;
+    } else {
+        p.part = off;
+        off += rup(Ssave * std::max(n_chunks * mxo, 256LL * (3 * q.Kl + 3)) * 4, 256);
+        p.bpart = off;
+        off += rup(Ssave * n_chunks * mxm * 4, 256);
+    }
     p.total = off;
+}
+
+// the weight-gradient launches of piece j of a pipelined step (second stream)
+static int wgrad_piece(const marf_net* net, const GeoDev& g, const Step2BufPlan& p, char* sv, int j, hipStream_t s2) {
+    const Step2NetPlan& q = net->s2;
+    const PipePlan& pp = p.pipe;
+    const int nl = net->n_layers;
+    const long long TPX = 32 * q.NW;
+    const long long t0 = (long long)j * pp.piece, t1 = std::min<long long>(p.n_tiles, t0 + pp.piece);
+    WgRange r;
+    r.s_lo = t0 * TPX;
+    r.s_len = (t1 - t0) * TPX;
+    r.n = j == pp.P - 1 ? pp.wg_last : pp.R;
+    r.part0 = j * pp.R;
+    const bool f0 = l0_recompute(net, g, p.S);
+    for (int l = 0; l < nl - 1; ++l) {
+        const int K = l == 0 ? q.ldf0 : net->Kp[l];
+        float* part = (float*)(sv + p.partl[l]);
+        float* bpart = (float*)(sv + p.bpartl[l]);
+        MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s2);
+        if (l == 0 && f0)
+            HIPCHK(marf_launch_wgrad_l0_recompute(sv + p.dz[1], net->Kp[1], g, (const float*)(sv + p.c2f), net->L, q.nk0,
+                                                  p.S, net->Mp[0], 32, r.n, part, bpart, s2, &r),
+                   "step_forward pipelined wgrad_l0");
+        else
+            HIPCHK(marf_launch_wgrad(1, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K, 32, r.n,
+                                     part, bpart, s2, &r),
+                   "step_forward pipelined wgrad");
+    }
+    return MARF_OK;
 }
 
 static int step2_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
@@ -907,13 +1064,39 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
         HIPCHK(marf_launch_step2(a, q.variant, p.grid, s), "render step2");
         return MARF_OK;
     }
-    {
+    double* const loss0 = a.loss_partial;
+    if (!p.pipe.on) {
         MarfProfScope ps("mlp_step", s);
         HIPCHK(marf_launch_step2(a, q.variant, p.grid, s), "step_forward step2");
+    } else {
+        // pieces of the step kernel on stream s, each followed by its weight gradients on s2
+        const PipePlan& pp = p.pipe;
+        PipeStreams* st = nullptr;
+        rc = pipe_streams(&st);
+        if (rc) return rc;
+        float* const blast0 = a.blast_partial;
+        float* const wlast0 = a.wlast_partial;
+        for (int j = 0; j < pp.P; ++j) {
+            a.tile0 = j * pp.piece;
+            a.n_tiles = std::min(p.n_tiles, (j + 1) * pp.piece);
+            a.loss_partial = loss0 + (size_t)j * pp.G * 2;
+            a.blast_partial = blast0 + (size_t)j * pp.G * 3;
+            a.wlast_partial = wlast0 + (size_t)j * pp.G * 3 * q.Kl;
+            {
+                MarfProfScope ps("mlp_step", s);
+                HIPCHK(marf_launch_step2(a, q.variant, pp.G, s), "step_forward step2 piece");
+            }
+            HIPCHK(hipEventRecord(st->ev[j], s), "pipeline: record");
+            HIPCHK(hipStreamWaitEvent(st->s2, st->ev[j], 0), "pipeline: wait");
+            rc = wgrad_piece(net, a.geo, p, sv, j, st->s2);
+            if (rc) return rc;
+        }
+        HIPCHK(hipEventRecord(st->ev[MARF_PIPE_MAXP], st->s2), "pipeline: record");
+        HIPCHK(hipStreamWaitEvent(s, st->ev[MARF_PIPE_MAXP], 0), "pipeline: join");
     }
     {
         MarfProfScope ps("loss_final", s);
-        HIPCHK(marf_launch_loss_final(a.loss_partial, p.grid, d_loss_out, d_denom_override, s), "step_forward loss");
+        HIPCHK(marf_launch_loss_final(loss0, p.nblk, d_loss_out, d_denom_override, s), "step_forward loss");
     }
     return MARF_OK;
 }
@@ -932,7 +1115,18 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
     float* bpart = (float*)(sv + p.bpart);
     const float* denom = d_loss_out + 1;
     const int nl = net->n_layers;
-    if (d_dparams) {
+    if (d_dparams && p.pipe.on) {  // the split-K partials were computed beside the step kernel
+        const int* kmap = (const int*)(sv + p.kmap);
+        for (int l = 0; l < nl - 1; ++l) {
+            const int K = l == 0 ? q.ldf0 : net->Kp[l];
+            MarfProfScope ps("wgrad_reduce", s);
+            HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.partl[l]), (const float*)(sv + p.bpartl[l]),
+                                            p.pipe.n_parts, net->Mp[l], K, net->dims[l + 1], net->dims[l],
+                                            d_dparams + net->w_off[l], d_dparams + net->b_off[l], s, d_gout, denom,
+                                            nullptr, l == 0 ? kmap : nullptr),
+                   "step_backward wgrad reduce (pipelined)");
+        }
+    } else if (d_dparams) {
         const long long chunk = wgrad_chunk(p.S);
         const int n_chunks = (int)((p.S + chunk - 1) / chunk);
         const int* kmap = (const int*)(sv + p.kmap);
@@ -958,9 +1152,11 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                        "step_backward wgrad reduce");
             }
         }
+    }
+    if (d_dparams) {
         const int l = nl - 1;
         MarfProfScope ps("wgrad_last_reduce", s);
-        HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.wlast), (const float*)(sv + p.blast), p.grid, 3, q.Kl, 3,
+        HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.wlast), (const float*)(sv + p.blast), p.nblk, 3, q.Kl, 3,
                                         net->dims[l], d_dparams + net->w_off[l], d_dparams + net->b_off[l], s, d_gout,
                                         denom, part),
                "step_backward last reduce");

@@ -106,7 +106,7 @@ struct Step2Args {
     const float* c2f_w;              // [L] band weights of this step
     float* dummy;                    // [grid][NW][ST][64][2] store sink
     unsigned long long* stamps;      // diagnostic builds (MARF_STAMPS): [grid][8] cycle totals of wave 0
-    int n_tiles;                     // block tiles of 32 * NW pixel slots
+    int tile0, n_tiles;              // this launch's block tiles [tile0, n_tiles) of 32 * NW pixel slots
     int fwd_only;                    // render: forward stages only, rgb out, nothing saved
     int feat0_recompute;             // feat_0 is recomputed by the layer-0 weight gradient: not stored
     const float* pro_fallback;       // valid device address for the input DMA when gt / H are absent
@@ -141,12 +141,20 @@ hipError_t marf_launch_reduce_dH(const float* partial, int tiles_per_patch, int 
                                  const float* denom = nullptr);
 hipError_t marf_launch_mlp_fwd(const marf::FwdArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
 hipError_t marf_launch_mlp_bwd(const marf::BwdArgs& a, int dtype, int TP, size_t lds, int n_tiles, hipStream_t s);
+// one piece of a pipelined step's weight gradients: n blocks split the pixel rows [s_lo, s_lo + s_len)
+// and write split-K partials part0 .. part0 + n - 1
+struct WgRange {
+    long long s_lo, s_len;
+    int n, part0;
+};
+bool marf_wgrad_range_ok(int dtype, int M, int ldz, int K, int ldf);
 bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk, int n_chunks, long long Np_pad);
 hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev& geo, const float* c2f_w, int L,
                                           int nk0, long long S, int M, int chunk, int n_chunks, float* partial,
-                                          float* bpartial, hipStream_t s);
+                                          float* bpartial, hipStream_t s, const WgRange* rng = nullptr);
 hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
-                             int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s);
+                             int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s,
+                             const WgRange* rng = nullptr);
 hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* feat, long long S, int ldf, int K,
                                   int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s);
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,

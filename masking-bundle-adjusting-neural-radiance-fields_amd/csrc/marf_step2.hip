@@ -205,8 +205,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
 
     const int tpp = a.geo.Np_pad / C::TPX;   // block tiles per patch
     const int Np = a.geo.Np;
+    // this launch's tiles: tile0 + blockIdx.x + i gridDim.x < n_tiles (one piece of a pipelined step,
+    // or all of them)
+    const int tbase = a.tile0 + (int)blockIdx.x;
     int my_tiles = 0;
-    if ((int)blockIdx.x < a.n_tiles) my_tiles = (a.n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
+    if (tbase < a.n_tiles) my_tiles = (a.n_tiles - 1 - tbase) / (int)gridDim.x + 1;
     // Stage order of a group of NS tiles: the forward stages of each tile, then ONE pass of the
     // dgrad stages for all of them (render: forward stages only)
     const int nF = a.n_fwd, nB = a.n_stages - a.n_fwd;
@@ -326,7 +329,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     };
 
     if (my_tiles > 0) {
-        issue_pro((int)blockIdx.x, 0);
+        issue_pro(tbase, 0);
         dma_arm();
         dma_burst();
         dma_arm();
@@ -670,7 +673,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         for (int si = 0; si < nset; ++si) {
             S2T_BEGIN(4);
             const int ti = it + si;
-            const int tile = (int)blockIdx.x + ti * (int)gridDim.x;
+            const int tile = tbase + ti * (int)gridDim.x;
             const int pb = ti & 1;
             const int b = tile / tpp;
             const int p0 = (tile - b * tpp) * C::TPX + 32 * wave;

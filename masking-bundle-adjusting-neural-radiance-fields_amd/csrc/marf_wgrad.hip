@@ -42,6 +42,11 @@ struct WgArgs {
     int n_oblk_c;      // output blocks along K
     float* partial;    // [n_chunks][M][K]
     float* bpartial;   // [n_chunks][M] (bias), may be null
+    // range mode (rng_n > 0, LDS-DMA kernel only): block c of rng_n reduces its share of the pixel
+    // rows [s_lo, s_lo + s_len) (whole SP-row stages, split as evenly as they go) into partial
+    // part0 + c -- one piece of a pipelined step (marf_abi.hip, step2_forward)
+    long long s_lo, s_len;
+    int rng_n, part0;
 };
 
 template <int RT, int CT>
@@ -273,8 +278,18 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         ob = blockIdx.x / a.n_chunks;
     }
     const int m0 = (ob / a.n_oblk_c) * 256, k0 = (ob % a.n_oblk_c) * KF;
-    const long long s_begin = (long long)chunk_id * a.chunk;
-    const long long s_end = min(s_begin + a.chunk, a.S);
+    long long s_begin, s_end;
+    int pidx;  // the partial this block writes
+    if (a.rng_n > 0) {
+        const long long nst = a.s_len / SP;
+        s_begin = a.s_lo + (long long)chunk_id * nst / a.rng_n * SP;
+        s_end = a.s_lo + (long long)(chunk_id + 1) * nst / a.rng_n * SP;
+        pidx = a.part0 + chunk_id;
+    } else {
+        s_begin = (long long)chunk_id * a.chunk;
+        s_end = min(s_begin + a.chunk, a.S);
+        pidx = chunk_id;
+    }
     const int n_st = s_end > s_begin ? (int)((s_end - s_begin) / SP) : 0;  // host: multiples of SP
     const bool do_bias = a.bpartial != nullptr && k0 == 0;
     const char* dz = reinterpret_cast<const char*>(a.dz) + (size_t)m0 * 2;
@@ -450,7 +465,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         }
     }
 
-    float* out = a.partial + (size_t)chunk_id * a.M * a.K + (size_t)m0 * a.K + k0;
+    float* out = a.partial + (size_t)pidx * a.M * a.K + (size_t)m0 * a.K + k0;
 #pragma unroll
     for (int i = 0; i < RT; ++i)
 #pragma unroll
@@ -465,7 +480,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         bs[threadIdx.x] = bsum;
         __syncthreads();
         if (threadIdx.x < 256)
-            a.bpartial[(size_t)chunk_id * a.M + m0 + threadIdx.x] = bs[threadIdx.x] + bs[threadIdx.x + 256];
+            a.bpartial[(size_t)pidx * a.M + m0 + threadIdx.x] = bs[threadIdx.x] + bs[threadIdx.x + 256];
     }
 }
 
@@ -660,8 +675,17 @@ static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
 // Picks the output-block shape for an M x K weight gradient: 256x256 (2x4 tiles per wave),
 // 256x64 (2x1) or 128x64 (1x1).
 hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
-                             int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s) {
+                             int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s,
+                             const WgRange* rng) {
     WgArgs a;
+    memset(&a, 0, sizeof(a));
+    if (rng) {
+        a.s_lo = rng->s_lo;
+        a.s_len = rng->s_len;
+        a.rng_n = n_chunks = rng->n;
+        a.part0 = rng->part0;
+        chunk = 32;  // (the stage granularity the range mode splits at)
+    }
     a.dz = dz;
     a.feat = feat;
     a.S = S;
@@ -684,6 +708,7 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
     const bool dma = M % 256 == 0 && ldz % 8 == 0 && ldz >= M && S % 32 == 0 && chunk % 32 == 0 &&
                      (long long)n_chunks * (M / 256) * ((K + 255) / 256) <= 0x7fffffff && wgrad_dma_enabled();
     const bool dma256 = dma && K % 256 == 0 && ldf % 8 == 0 && ldf >= K, dma96 = dma && K == 96 && ldf == 96;
+    if (rng && (dtype == 0 || !(dma256 || dma96))) return hipErrorInvalidValue;  // range mode: LDS-DMA kernel only
     if (dtype == 1) {
         if (dma256) return launch_wg_dma<PrecBF16, 256>(a, n_chunks, s);
         if (dma96) return launch_wg_dma<PrecBF16, 96>(a, n_chunks, s);
@@ -706,6 +731,14 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
     return launch_wg<PrecF32, 1, 1>(a, n_chunks, nr * nc, s);
 }
 
+// The range mode (WgRange) runs on the LDS-DMA kernel only: true if an M x K gradient with these
+// strides takes it (bf16 / fp16; marf_launch_wgrad's dma256 / dma96 conditions).
+bool marf_wgrad_range_ok(int dtype, int M, int ldz, int K, int ldf) {
+    if (dtype != 1 && dtype != 2) return false;
+    if (!(M % 256 == 0 && ldz % 8 == 0 && ldz >= M && wgrad_dma_enabled())) return false;
+    return (K % 256 == 0 && ldf % 8 == 0 && ldf >= K) || (K == 96 && ldf == 96);
+}
+
 // Layer-0 weight gradient with feat_0 recomputed on chip (step kernel's feat0_recompute); bf16,
 // 256-wide layer 0, the 96-wide feat_0 of L = 13..16.  False if the shape does not qualify.
 bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk, int n_chunks, long long Np_pad) {
@@ -715,9 +748,15 @@ bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk
 
 hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev& geo, const float* c2f_w, int L,
                                           int nk0, long long S, int M, int chunk, int n_chunks, float* partial,
-                                          float* bpartial, hipStream_t s) {
+                                          float* bpartial, hipStream_t s, const WgRange* rng) {
     WgArgs a;
     memset(&a, 0, sizeof(a));
+    if (rng) {
+        a.s_lo = rng->s_lo;
+        a.s_len = rng->s_len;
+        a.rng_n = n_chunks = rng->n;
+        a.part0 = rng->part0;
+    }
     a.dz = dz;
     a.feat = nullptr;
     a.f0.geo = geo;

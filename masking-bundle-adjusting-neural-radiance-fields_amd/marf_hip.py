@@ -49,6 +49,7 @@ _SIGS = {
     "marf_net_param_count": (_c_ll, [_c_vp]),
     "marf_net_packed_bytes": (_c_sz, [_c_vp]),
     "marf_net_pack": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp]),
+    "marf_net_set_pipeline": (_c_int, [_c_vp, _c_int, _c_int, _c_int]),
     "marf_saved_bytes": (_c_sz, [_c_vp, ctypes.POINTER(Geometry)]),
     "marf_workspace_bytes": (_c_sz, [_c_vp, ctypes.POINTER(Geometry)]),
     "marf_forward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_vp, _c_vp, _c_vp, _c_vp]),
@@ -369,6 +370,12 @@ class Net:
 
     def pack(self, flat_params, packed):
         _check(lib().marf_net_pack(self._h, _ptr(flat_params), _ptr(packed), _stream(flat_params)))
+
+    def set_pipeline(self, mode=-1, wg_blocks=0, piece_tiles=0):
+        """Pipelined weight gradients of the fused step (include/marf.h marf_net_set_pipeline):
+        mode 0 off (default: measured slower), 1 on at any size, -1 large steps
+        only.  Between steps only."""
+        _check(lib().marf_net_set_pipeline(self._h, int(mode), int(wg_blocks), int(piece_tiles)))
 
     def saved_bytes(self, geo):
         return lib().marf_saved_bytes(self._h, ctypes.byref(geo))

@@ -597,6 +597,61 @@ def test_step2_tile_grouping_invariance(grid, tmp_path):
     assert abs(l0 - l1) <= 1e-6 * abs(l0)
 
 
+@pytest.mark.parametrize("wg,piece", [(28, 0), (5, 512), (100, 2046)])
+def test_pipelined_step_matches_one_launch(wg, piece, tmp_path):
+    """Pipelined weight gradients (include/marf.h marf_net_set_pipeline): the bf16x3 step kernel in
+    pieces of whole tiles on CUs - wg blocks, each piece's hidden / layer-0 weight-gradient partials
+    on wg blocks of a second stream while the next piece runs.  Against the one-launch step on the
+    same state: rgb and the warp gradient are per-pixel results, bit-identical; the weight gradients
+    are the same sums split into other split-K chunks (and the last layer's into other block
+    partials), so they agree to fp32 summation order (<= 1e-5 of each tensor's max); the loss to
+    1e-6.  Reruns are bit-identical and the gradients scale exactly with d loss."""
+    from model import planar
+    from util import EasyDict as edict
+    B = 6  # 3072 tiles: pieces of 2 x (CUs - wg) tiles by default (P = 7 at 256 CUs), 512 (P = 6), 2046 (P = 2)
+    opt = make_opt(tmp_path, H=512, W=512, patch_H=256, patch_W=256, batch_size=B, precision="bf16x3",
+                   arch={"layers": [None, 256, 256, 256, 256, 3], "skip": [], "posenc": {"L_2D": 16}})
+    torch.manual_seed(0)
+    graph = planar.Graph(opt).to(DEV)
+    graph.neural_image.progress.data.fill_(0.2)
+    rng = np.random.default_rng(6)
+    gt = t(rng.random((B, 3, 256, 256)).astype(np.float32))
+    mask = t((rng.random((B, 1, 256, 256)) < 0.85).astype(np.float32))
+    var = edict(images=edict(rgb=gt, masks=mask, masks_eroded=mask, edges=None))
+    graph.need_edges = False
+    with torch.no_grad():
+        graph.warp_param.weight.copy_(t((rng.standard_normal((B, 8)) * 0.01).astype(np.float32)))
+    net = graph.neural_image.engine(torch.device(DEV)).net
+
+    def run(scale=1.0):
+        for q in graph.parameters():
+            q.grad = None
+        v = graph.forward(var)
+        loss = graph.compute_loss(v).rgb
+        (loss * scale).backward()
+        return (float(loss.detach()), v.rgb_prediction.detach().clone(),
+                [q.grad.clone() for q in graph.neural_image.mlp.parameters()], graph.warp_param.weight.grad.clone())
+
+    net.set_pipeline(0)
+    l0, rgb0, g0, w0 = run()
+    net.set_pipeline(1, wg, piece)
+    try:
+        l1, rgb1, g1, w1 = run()
+        l2, rgb2, g2, w2 = run()
+        l3, _, g3, w3 = run(2.0)
+    finally:
+        net.set_pipeline(-1)
+    assert torch.equal(rgb0, rgb1) and torch.equal(w0, w1)
+    for i, (a, b) in enumerate(zip(g0, g1)):
+        assert torch.isfinite(b).all()
+        err = float((a - b).abs().max())
+        assert err <= 1e-5 * float(a.abs().max()), (i, err, float(a.abs().max()))
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+    assert l1 == l2 and torch.equal(rgb1, rgb2) and torch.equal(w1, w2)
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+    assert l3 == l1 and torch.equal(2 * w1, w3) and all(torch.equal(2 * a, b) for a, b in zip(g1, g3))
+
+
 def test_wgrad_dma_wide_layers_bitwise(tmp_path):
     """512-wide hidden layers (C5 shape): the LDS-DMA weight-gradient kernel splits each output in
     256 x 256 blocks (and layer 0 in 256 x 96 blocks); its gradients equal the register-staged
