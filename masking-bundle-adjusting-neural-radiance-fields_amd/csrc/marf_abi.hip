@@ -45,8 +45,12 @@ static inline long long rup(long long x, long long m) { return (x + m - 1) / m *
 
 // step2 plan (the pixel-per-wave fused step, marf_step2.hip), filled by plan_step2_net
 struct Step2NetPlan {
-    int variant;           // -1: not available for this net; 0: bf16 (8 waves); 1: split bf16 (4 waves)
+    int variant;           // -1: not available for this net; 0: bf16 (8 waves); 1: split bf16 (4 waves);
+                           // 3: split bf16, two waves per SIMD (marf_step3.hip)
     int NW, NS, HM, MAXR, NMW, slot, nk0, nta, n_stages, nbias, Kl, ldf0;
+    int PX, TPX;           // pixels per wave, pixel slots per block tile
+    int nk0w;              // k_step2's layer-0 k-steps: feat_0's column layout (weight gradient, kmap)
+    int n_fwd;             // the program's forward stages
     int r0, ns0;           // layer-0 row tiles per stage (their k-steps share one slot) and its stages
     int nrt[MARF_MAX_LAYERS], nrtb[MARF_MAX_LAYERS], boff[MARF_MAX_LAYERS];
     size_t prog_off, bias_off, kmap_off, end_off;
@@ -91,6 +95,52 @@ static bool step2_env_enabled() {
     return e && e[0] == '1';
 }
 
+int marf_step3_wave_lds_bytes();
+
+// variant 3 (marf_step3.hip): 16 pixels per wave on 16x16x32 MFMAs, 8 waves, 32 KB stages of
+// 16-row tiles -- layer 0: r0 row tiles of nk0 k-steps (nb = ceil(L / 8) band steps + the raw
+// coordinates); hidden / adjoint: two row tiles of 8 k-steps; the last-layer dgrad: every row tile
+static void plan_step3_net(marf_net* n) {
+    Step2NetPlan& q = n->s2;
+    const int nl = n->n_layers;
+    q.variant = 3;
+    q.HM = 256;
+    q.NW = 8;
+    q.NS = 1;
+    q.PX = 16;
+    q.TPX = 128;
+    q.MAXR = 4;
+    q.NMW = 4;
+    q.slot = 32768;
+    const int nb = (n->L + 7) / 8;
+    q.nk0 = nb + 1;
+    q.nta = 2 * nb + 1;
+    q.nk0w = (n->L + 3) / 4 + 1;
+    q.ldf0 = (int)rup(16 * q.nk0w, 32);
+    q.Kl = n->Kp[nl - 1];
+    int bo = 0;
+    for (int l = 0; l < nl; ++l) {
+        q.nrt[l] = l == nl - 1 ? 1 : n->Mp[l] / 16;
+        q.nrtb[l] = l == 0 ? q.nta : n->Kp[l] / 16;
+        q.boff[l] = bo;
+        bo += l == nl - 1 ? 32 : n->Mp[l];
+    }
+    q.nbias = bo;
+    q.r0 = std::max(2, (16 / q.nk0) & ~1);
+    q.ns0 = (q.nrt[0] + q.r0 - 1) / q.r0;
+    int st = q.ns0;
+    for (int l = 1; l < nl - 1; ++l) st += q.nrt[l] / 2;
+    q.n_fwd = st + 1;
+    st += 2;
+    for (int l = nl - 2; l >= 1; --l) st += q.nrtb[l] / 2;
+    st += (q.nta + 1) / 2;
+    q.n_stages = st;
+    q.prog_off = rup((long long)n->packed_bytes, 4096);
+    q.bias_off = q.prog_off + (size_t)st * q.slot;
+    q.kmap_off = rup((long long)(q.bias_off + (size_t)q.nbias * 4), 256);
+    q.end_off = rup((long long)(q.kmap_off + (size_t)n->D * 4), 256);
+}
+
 // Which pixel-per-wave variant (marf_step2.hip) runs this net, its weight-program shape and the
 // byte layout of the program / bias table / layer-0 column map appended to the packed buffer.
 static void plan_step2_net(marf_net* n) {
@@ -106,16 +156,26 @@ static void plan_step2_net(marf_net* n) {
     if (n->dtype != MARF_BF16X3 && !step2_env_enabled()) return;
     q.HM = 256;
     q.variant = n->dtype == MARF_BF16X3 ? 1 : 0;
+    if (q.variant == 1) {  // the two-waves-per-SIMD kernel: MARF_STEP3=1 at net creation (in development)
+        const char* e = getenv("MARF_STEP3");
+        if (e && e[0] == '1') {
+            plan_step3_net(n);
+            return;
+        }
+    }
     {
         const char* e = getenv("MARF_STEP2_NW4");  // diagnostic: plain bf16 on 4 waves per block
         if (q.variant == 0 && e && e[0] == '1') q.variant = 2;
     }
     q.NW = q.variant == 0 ? 8 : 4;
     q.NS = q.variant == 1 ? 2 : 1;  // pixel sets per dgrad pass (S2Cfg::NS)
+    q.PX = 32;
+    q.TPX = 32 * q.NW;
     q.MAXR = 4;
     q.NMW = q.HM / 64;
     q.slot = (q.HM / 16) * 1024 * (q.variant == 1 ? 2 : 1);
     q.nk0 = (n->L + 3) / 4 + 1;
+    q.nk0w = q.nk0;
     q.nta = (2 * n->L + 1 + 15) / 16;
     q.ldf0 = (int)rup(16 * q.nk0, 32);
     q.Kl = n->Kp[nl - 1];
@@ -131,6 +191,7 @@ static void plan_step2_net(marf_net* n) {
     q.ns0 = (q.nrt[0] + q.r0 - 1) / q.r0;
     st += q.ns0;
     for (int l = 1; l < nl - 1; ++l) st += q.nrt[l];
+    q.n_fwd = st + 1;
     st += 2;  // last layer forward, last-layer dgrad (every row tile in one stage)
     for (int l = nl - 2; l >= 1; --l) st += q.nrtb[l];
     st += q.nta;
@@ -493,9 +554,14 @@ int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, vo
         }
         b.nbias = q.nbias;
         char* pk = (char*)d_packed;
-        HIPCHK(marf_launch_pack2(d_params, pk + q.prog_off, (float*)(pk + q.bias_off), (int*)(pk + q.kmap_off), b,
-                                 (hipStream_t)stream),
-               "net_pack step2");
+        if (q.variant == 3)
+            HIPCHK(marf_launch_pack3(d_params, pk + q.prog_off, (float*)(pk + q.bias_off), (int*)(pk + q.kmap_off), b,
+                                     (hipStream_t)stream),
+                   "net_pack step3");
+        else
+            HIPCHK(marf_launch_pack2(d_params, pk + q.prog_off, (float*)(pk + q.bias_off), (int*)(pk + q.kmap_off), b,
+                                     (hipStream_t)stream),
+                   "net_pack step2");
     }
     return MARF_OK;
 }
@@ -801,7 +867,7 @@ static long long wgrad_chunk(long long S) {
 static bool l0_recompute(const marf_net* n, const GeoDev& g, long long S) {
     const char* e = getenv("MARF_F0_RECOMPUTE");
     if (e && e[0] == '0') return false;
-    if (n->s2.variant != 1 || g.mode != MARF_GEO_GRID) return false;
+    if ((n->s2.variant != 1 && n->s2.variant != 3) || g.mode != MARF_GEO_GRID) return false;
     const long long chunk = wgrad_chunk(S);
     return marf_wgrad_l0_recompute_ok(n->Mp[0], n->Kp[1], n->s2.ldf0, S, (int)chunk, (int)((S + chunk - 1) / chunk),
                                       g.Np_pad);
@@ -849,7 +915,7 @@ static void plan_pipe(const marf_net* n, const GeoDev& g, long long S, int n_til
         if (!marf_wgrad_range_ok(n->kdt, n->Mp[l], n->Kp[l + 1], n->Kp[l], n->Kp[l])) return;
     if (!marf_wgrad_range_ok(n->kdt, n->Mp[0], n->Kp[1], q.ldf0, q.ldf0)) return;
     if (l0_recompute(n, g, S)) {  // the recomputing kernel's ranges may span only a few patches
-        const long long mx = rup((long long)piece * 32 * q.NW / R + 32, 32);
+        const long long mx = rup((long long)piece * q.TPX / R + 32, 32);
         if (!marf_wgrad_l0_recompute_ok(n->Mp[0], n->Kp[1], q.ldf0, S, (int)mx, P * cus, g.Np_pad)) return;
     }
     pp.on = 1;
@@ -889,7 +955,7 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
     const int nl = n->n_layers;
     const long long Ssave = render ? 0 : 1;
     p.S = (long long)g.B * g.Np_pad;
-    p.n_tiles = (int)(p.S / (32 * q.NW));
+    p.n_tiles = (int)(p.S / q.TPX);
     int cap = device_cus();
     if (const char* e = getenv("MARF_STEP2_GRID")) cap = std::max(1, atoi(e));  // diagnostic override
     p.grid = std::max(1, std::min(p.n_tiles, cap));
@@ -905,13 +971,13 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
     p.dz[0] = 0;
     // dz_l and the dH partials carry 32 NW sink rows past S: the dgrad pass of a pixel set that has
     // no tile (an odd tile count with two sets per dgrad pass) stores there
-    const long long Ssink = p.S + 32 * q.NW;
+    const long long Ssink = p.S + q.TPX;
     for (int l = 1; l < nl; ++l) {
         p.dz[l] = off;
         off += rup(Ssave * Ssink * n->Kp[l] * 2, 256);
     }
     p.dH = off;
-    off += rup(Ssave * Ssink / 32 * 9 * 4, 256);
+    off += rup(Ssave * Ssink / q.PX * 9 * 4, 256);
     p.loss = off;
     off += rup((long long)p.nblk * 2 * 8, 256);
     p.blast = off;
@@ -919,7 +985,7 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
     p.wlast = off;
     off += rup((long long)p.nblk * 3 * q.Kl * 4, 256);
     p.dummy = off;
-    off += rup((long long)p.grid * q.NW * 4 * 64 * 2 * 4, 256);
+    off += rup((long long)p.grid * q.NW * 4096, 256);  // 64 B per lane
     p.c2f = off;
     off += 256;
     p.kmap = off;  // the layer-0 column map, copied from the packed buffer by the forward
@@ -958,7 +1024,7 @@ static int wgrad_piece(const marf_net* net, const GeoDev& g, const Step2BufPlan&
     const Step2NetPlan& q = net->s2;
     const PipePlan& pp = p.pipe;
     const int nl = net->n_layers;
-    const long long TPX = 32 * q.NW;
+    const long long TPX = q.TPX;
     const long long t0 = (long long)j * pp.piece, t1 = std::min<long long>(p.n_tiles, t0 + pp.piece);
     WgRange r;
     r.s_lo = t0 * TPX;
@@ -972,7 +1038,7 @@ static int wgrad_piece(const marf_net* net, const GeoDev& g, const Step2BufPlan&
         float* bpart = (float*)(sv + p.bpartl[l]);
         MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s2);
         if (l == 0 && f0)
-            HIPCHK(marf_launch_wgrad_l0_recompute(sv + p.dz[1], net->Kp[1], g, (const float*)(sv + p.c2f), net->L, q.nk0,
+            HIPCHK(marf_launch_wgrad_l0_recompute(sv + p.dz[1], net->Kp[1], g, (const float*)(sv + p.c2f), net->L, q.nk0w,
                                                   p.S, net->Mp[0], 32, r.n, part, bpart, s2, &r),
                    "step_forward pipelined wgrad_l0");
         else
@@ -983,13 +1049,17 @@ static int wgrad_piece(const marf_net* net, const GeoDev& g, const Step2BufPlan&
     return MARF_OK;
 }
 
+static hipError_t launch_s2(const Step2Args& a, int variant, int grid, hipStream_t s) {
+    return variant == 3 ? marf_launch_step3(a, grid, s) : marf_launch_step2(a, variant, grid, s);
+}
+
 static int step2_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
                          const float* d_gt, const float* d_mask, const float* d_denom_override, float* d_rgb,
                          float* d_loss_out, void* d_saved, hipStream_t s, bool render = false) {
     const Step2NetPlan& q = net->s2;
     Step2Args a;
     memset(&a, 0, sizeof(a));
-    int rc = make_geo(geo, a.geo, 32 * q.NW);
+    int rc = make_geo(geo, a.geo, q.TPX);
     if (rc) return rc;
     Step2BufPlan p;
     plan_step2_bufs(net, a.geo, p, render);
@@ -1006,8 +1076,7 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     a.prog = pk + q.prog_off;
     a.n_stages = q.n_stages;
     // the program's forward prefix: the layer-0 and hidden row tiles + the last layer
-    a.n_fwd = 1 + q.ns0;
-    for (int l = 1; l < nl - 1; ++l) a.n_fwd += q.nrt[l];
+    a.n_fwd = q.n_fwd;
     a.S = p.S;
     if (render) {
         a.fwd_only = 1;
@@ -1040,7 +1109,7 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     a.stamps = g_stamps;
     a.n_tiles = p.n_tiles;
     // LDS layout
-    const int TPX = 32 * q.NW;
+    const int TPX = q.TPX;
     int off = 3 * q.slot;
     a.lds_pro = off;
     off += 2 * (4 * TPX + 64) * 4;
@@ -1052,7 +1121,8 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     off += (int)sizeof(S2Layer) * MARF_MAX_LAYERS;
     a.lds_wave = off;
     // per wave: transpose + g^T scratch, ReLU mask words of each pixel set of a dgrad pass, dW_last
-    a.lds_wave_bytes = (int)rup(2048 + q.NS * q.MAXR * q.NMW * 256 + 12 * q.Kl, 16);
+    a.lds_wave_bytes = q.variant == 3 ? marf_step3_wave_lds_bytes()
+                                      : (int)rup(2048 + q.NS * q.MAXR * q.NMW * 256 + 12 * q.Kl, 16);
     off += q.NW * a.lds_wave_bytes;
     a.lds_total = off;
     if (off > 160 * 1024) return fail(MARF_ERR_UNSUPPORTED, "step2: LDS plan %d B exceeds 160 KB", off);
@@ -1061,13 +1131,13 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
            "step_forward kmap");
     if (render) {
         MarfProfScope ps("mlp_fwd", s);
-        HIPCHK(marf_launch_step2(a, q.variant, p.grid, s), "render step2");
+        HIPCHK(launch_s2(a, q.variant, p.grid, s), "render step2");
         return MARF_OK;
     }
     double* const loss0 = a.loss_partial;
     if (!p.pipe.on) {
         MarfProfScope ps("mlp_step", s);
-        HIPCHK(marf_launch_step2(a, q.variant, p.grid, s), "step_forward step2");
+        HIPCHK(launch_s2(a, q.variant, p.grid, s), "step_forward step2");
     } else {
         // pieces of the step kernel on stream s, each followed by its weight gradients on s2
         const PipePlan& pp = p.pipe;
@@ -1084,7 +1154,7 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
             a.wlast_partial = wlast0 + (size_t)j * pp.G * 3 * q.Kl;
             {
                 MarfProfScope ps("mlp_step", s);
-                HIPCHK(marf_launch_step2(a, q.variant, pp.G, s), "step_forward step2 piece");
+                HIPCHK(launch_s2(a, q.variant, pp.G, s), "step_forward step2 piece");
             }
             HIPCHK(hipEventRecord(st->ev[j], s), "pipeline: record");
             HIPCHK(hipStreamWaitEvent(st->s2, st->ev[j], 0), "pipeline: wait");
@@ -1106,7 +1176,7 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                           float* d_dparams, float* d_dh, hipStream_t s) {
     const Step2NetPlan& q = net->s2;
     GeoDev g;
-    int rc = make_geo(geo, g, 32 * q.NW);
+    int rc = make_geo(geo, g, q.TPX);
     if (rc) return rc;
     Step2BufPlan p;
     plan_step2_bufs(net, g, p);
@@ -1137,7 +1207,7 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                 MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
                 if (l == 0 && f0)
                     HIPCHK(marf_launch_wgrad_l0_recompute(sv + p.dz[1], net->Kp[1], g, (const float*)(sv + p.c2f), net->L,
-                                                          q.nk0, p.S, net->Mp[0], (int)chunk, n_chunks, part, bpart, s),
+                                                          q.nk0w, p.S, net->Mp[0], (int)chunk, n_chunks, part, bpart, s),
                            "step_backward wgrad_l0 (feat_0 recomputed)");
                 else
                     HIPCHK(marf_launch_wgrad(1, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K,
@@ -1163,7 +1233,7 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
     }
     if (d_dh) {
         MarfProfScope ps("warp_bwd", s);
-        HIPCHK(marf_launch_reduce_dH((const float*)(sv + p.dH), g.Np_pad / 32, g.B, d_h_params, nullptr, d_dh,
+        HIPCHK(marf_launch_reduce_dH((const float*)(sv + p.dH), g.Np_pad / q.PX, g.B, d_h_params, nullptr, d_dh,
                                      lie_batch > 0 ? lie_batch : g.B, s, d_gout, denom),
                "step_backward warp");
     }
@@ -1173,7 +1243,7 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
 size_t marf_render_workspace_bytes(const marf_net* net, const marf_geometry* geo) {
     if (!net || !geo || !use_step2(net)) return 0;
     GeoDev g;
-    if (make_geo(geo, g, 32 * net->s2.NW) != MARF_OK) return 0;
+    if (make_geo(geo, g, net->s2.TPX) != MARF_OK) return 0;
     Step2BufPlan p;
     plan_step2_bufs(net, g, p, true);
     return p.total;
@@ -1197,7 +1267,7 @@ size_t marf_step_saved_bytes(const marf_net* net, const marf_geometry* geo) {
     GeoDev g;
     if (!net || !geo || geo->mode == MARF_GEO_COORDS) return 0;
     if (use_step2(net)) {
-        if (make_geo(geo, g, 32 * net->s2.NW) != MARF_OK) return 0;
+        if (make_geo(geo, g, net->s2.TPX) != MARF_OK) return 0;
         Step2BufPlan p2;
         plan_step2_bufs(net, g, p2);
         return p2.total;
