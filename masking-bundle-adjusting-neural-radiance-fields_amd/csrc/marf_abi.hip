@@ -1049,8 +1049,12 @@ static int wgrad_piece(const marf_net* net, const GeoDev& g, const Step2BufPlan&
     return MARF_OK;
 }
 
-static hipError_t launch_s2(const Step2Args& a, int variant, int grid, hipStream_t s) {
-    return variant == 3 ? marf_launch_step3(a, grid, s) : marf_launch_step2(a, variant, grid, s);
+static hipError_t launch_s2(const marf_net* n, const Step2Args& a, int grid, hipStream_t s) {
+    const Step2NetPlan& q = n->s2;
+    if (q.variant != 3) return marf_launch_step2(a, q.variant, grid, s);
+    bool full = n->L >= 1;  // every hidden layer 256 wide
+    for (int l = 0; l < n->n_layers - 1; ++l) full = full && n->Mp[l] == 256;
+    return marf_launch_step3(a, full, grid, s);
 }
 
 static int step2_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
@@ -1131,13 +1135,13 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
            "step_forward kmap");
     if (render) {
         MarfProfScope ps("mlp_fwd", s);
-        HIPCHK(launch_s2(a, q.variant, p.grid, s), "render step2");
+        HIPCHK(launch_s2(net, a, p.grid, s), "render step2");
         return MARF_OK;
     }
     double* const loss0 = a.loss_partial;
     if (!p.pipe.on) {
         MarfProfScope ps("mlp_step", s);
-        HIPCHK(launch_s2(a, q.variant, p.grid, s), "step_forward step2");
+        HIPCHK(launch_s2(net, a, p.grid, s), "step_forward step2");
     } else {
         // pieces of the step kernel on stream s, each followed by its weight gradients on s2
         const PipePlan& pp = p.pipe;
@@ -1154,7 +1158,7 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
             a.wlast_partial = wlast0 + (size_t)j * pp.G * 3 * q.Kl;
             {
                 MarfProfScope ps("mlp_step", s);
-                HIPCHK(launch_s2(a, q.variant, pp.G, s), "step_forward step2 piece");
+                HIPCHK(launch_s2(net, a, pp.G, s), "step_forward step2 piece");
             }
             HIPCHK(hipEventRecord(st->ev[j], s), "pipeline: record");
             HIPCHK(hipStreamWaitEvent(st->s2, st->ev[j], 0), "pipeline: wait");

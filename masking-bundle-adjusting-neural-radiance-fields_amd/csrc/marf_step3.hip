@@ -42,8 +42,7 @@ constexpr int SLOT = 32768;                   // one ring slot = one program sta
 constexpr int LO = 16384;                     // byte offset of the lo fragments in a slot
 constexpr int PER_DMA = SLOT / (NW * 1024);   // 1 KB DMA pieces per wave and stage
 constexpr int NSLOT = 3;
-constexpr int NK0 = 5;                        // max layer-0 k-steps (L <= 32: 4 band steps + raw)
-constexpr int NTA = 2 * (NK0 - 1) + 1;        // max adjoint row tiles
+constexpr int NK0MAX = 5;                     // max layer-0 k-steps (L <= 32: 4 band steps + raw)
 constexpr int NML = 4;                        // max ReLU layers (nl <= 5)
 // wave-private LDS: g^T image (256 B), transpose scratch (1 KB), mask words [NML][2][64], dW_last [3][256]
 constexpr int W_GIMG = 0, W_SCR = 256, W_MASK = 1280, W_WLA = W_MASK + NML * 2 * 64 * 4;
@@ -154,13 +153,21 @@ MARF_DEV uint2 s3_bwd_ep(const f32x4& acc, uint32_t mw) {
 
 // ------------------------------------------------------------------ the kernel
 
+// NK0T: layer-0 k-steps (nb + 1 = ceil(L / 8) + 1); FULL: every hidden layer 256 wide.  Both make
+// the row-tile and k-step counts compile-time (no guards, no merges of partly written operand
+// arrays, which cost registers); <NK0MAX, false> is the generic instantiation.
+template <int NK0T, bool FULL>
 __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
     using namespace s3;
+    constexpr int NK0 = NK0T;
+    constexpr int NTA = 2 * (NK0 - 1) + 1;        // adjoint row tiles (max)
+    constexpr int R0F = (16 / NK0) & ~1;           // layer-0 row tiles per stage (FULL)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pxl = lane & 15, grp = lane >> 4;
-    const int nl = a.nl, L = a.L, nk0 = a.nk0, nb = a.nk0 - 1;
+    const int nl = a.nl, L = a.L;
+    const int nk0 = FULL ? NK0 : a.nk0, nb = nk0 - 1;
 
     const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
     float* bias_l = reinterpret_cast<float*>(smem + a.lds_bias);
@@ -293,24 +300,32 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
             A0[1] = ah[64];
             A1[1] = al[64];
         }
+        // sched_barrier pins the order: left alone the scheduler sinks each LDS read to right before
+        // its MFMA (an lgkmcnt(0) wait per MFMA) to save the ring's registers
+        __builtin_amdgcn_sched_barrier(0);
         s3_sfor<NK>([&](auto ksc) {
             constexpr int ks = decltype(ksc)::value;
-            const bf16x8 x = A0[ks & 1], y = A1[ks & 1];
-            if constexpr (ks + 2 < NK) {
-                A0[ks & 1] = ah[(ks + 2) * 64];
-                A1[ks & 1] = al[(ks + 2) * 64];
-            }
+            constexpr int u = ks & 1;
             const bool live = NK != NK0 || ks < nk;
             if (live) {
                 if constexpr (MODE == 1) {
-                    mf(acc, x, Bh[ks].f);
-                    mf(acc, x, Bl[ks].f);
-                    mf(acc, y, Bh[ks].f);
+                    mf(acc, A0[u], Bh[ks].f);
+                    mf(acc, A0[u], Bl[ks].f);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (ks + 2 < NK) A0[u] = ah[(ks + 2) * 64];
+                    mf(acc, A1[u], Bh[ks].f);
                 } else {
-                    mf(acc, x, Bh[ks].f);
-                    mf(acc, y, Bh[ks].f);
+                    mf(acc, A0[u], Bh[ks].f);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (ks + 2 < NK) A0[u] = ah[(ks + 2) * 64];
+                    mf(acc, A1[u], Bh[ks].f);
                 }
+            } else if constexpr (ks + 2 < NK) {
+                A0[u] = ah[(ks + 2) * 64];
             }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ks + 2 < NK) A1[u] = al[(ks + 2) * 64];
+            __builtin_amdgcn_sched_barrier(0);
         });
     };
     typedef std::integral_constant<int, 1> MFt;
@@ -348,9 +363,6 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         const float* pro = pro_buf(pb);
 
         // ---- prologue: pixel grid -> warp (warp.py:33-81) -> posenc + c2f (model/planar.py:451-471)
-        float Hm[9];
-#pragma unroll
-        for (int e = 0; e < 9; ++e) Hm[e] = pro[4 * TPX + e];
         float u, v, X[3];
         if (a.geo.mode == 1) {  // explicit coordinates (render only)
             const int pc = min(p, Np - 1);
@@ -363,7 +375,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
             const int r = p / a.geo.w, cc = p - r * a.geo.w;
             const float x = grid_coord(a.geo.x0 + cc, a.geo.W, a.geo.norm_w);
             const float y = grid_coord(a.geo.y0 + r, a.geo.H, a.geo.norm_h);
-            warp_point(Hm, x, y, u, v, X, a.geo.bmm_small);
+            warp_point(pro + 4 * TPX, x, y, u, v, X, a.geo.bmm_small);
         }
         {
             // layer-0 operand: band k-step ks, group g: bands 8 ks + 4 (g >> 1) + 0..3 of coordinate
@@ -424,7 +436,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         // ---- forward: layer 0, hidden layers.  Row tile rt of layer l: acc = bias + W . B, epilogue,
         //      the pair (2s, 2s + 1) -> operand k-step s of layer l + 1 (+ feat_{l+1} store, mask words)
         auto fwd_layer = [&](int l, const S3Frag* BH, const S3Frag* BL, int nk, auto nk_tag, int r0) {
-            const int nrt = ly_int(l, 0);
+            const int nrt = FULL ? (l == 0 ? NRT : NRT) : ly_int(l, 0);
             const bool save = l + 1 < nl - 1 && !a.fwd_only;
             u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) : nullptr;
             const int boff = ly_int(l, 2);
@@ -466,7 +478,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                 Bl[k] = Ol[k];
             }
         };
-        fwd_layer(0, Bh, Bl, nk0, NK0t(), a.r0);
+        fwd_layer(0, Bh, Bl, nk0, NK0t(), FULL ? R0F : a.r0);
         for (int l = 1; l < nl - 1; ++l) fwd_layer(l, Bh, Bl, NKH, NKHt(), 2);
 
         // ---- last layer: 3 outputs (rows 0..2 of one tile, lanes 0..15), sigmoid, masked MSE, d rgb
@@ -608,16 +620,16 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         };
         {
             const char* slot = stage_begin();
-            bwd_pass(nl - 1, nl - 2, ly_int(nl - 1, 1), slot, true);
+            bwd_pass(nl - 1, nl - 2, FULL ? NRT : ly_int(nl - 1, 1), slot, true);
         }
-        for (int l = nl - 2; l >= 1; --l) bwd_pass(l, l - 1, ly_int(l, 1), nullptr, false);
+        for (int l = nl - 2; l >= 1; --l) bwd_pass(l, l - 1, FULL ? NRT : ly_int(l, 1), nullptr, false);
 
         // ---- layer-0 dgrad + posenc adjoint: row tile t, register r of lane group G holds band
         //      4 t + r of coordinate G >> 1, the sin slot for even G, the cos slot for odd G (the raw
         //      coordinates: tile 2 nb, register 0 of groups 0 (u) and 2 (v))
         float dc = 0.f;
         {
-            const int nta = a.nta;
+            const int nta = FULL ? NTA : a.nta;
             const float cd = (grp >> 1) ? v : u;
             const char* slot = nullptr;
             s3_sfor<NTA>([&](auto tc) {
@@ -867,11 +879,19 @@ __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog
 
 using namespace marf;
 
-hipError_t marf_launch_step3(const Step2Args& a, int grid, hipStream_t s) {
-    hipError_t e = ensure_dynamic_lds((const void*)k_step3, (size_t)a.lds_total);
+template <int NK0T, bool FULL>
+static hipError_t launch_step3_t(const Step2Args& a, int grid, hipStream_t s) {
+    hipError_t e = ensure_dynamic_lds((const void*)k_step3<NK0T, FULL>, (size_t)a.lds_total);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_step3, dim3(grid), dim3(s3::NW * 64), (size_t)a.lds_total, s, a);
+    hipLaunchKernelGGL((k_step3<NK0T, FULL>), dim3(grid), dim3(s3::NW * 64), (size_t)a.lds_total, s, a);
     return hipGetLastError();
+}
+
+// full = every hidden layer 256 wide (the host checks): L <= 8 and L <= 16 get their own code
+hipError_t marf_launch_step3(const Step2Args& a, bool full, int grid, hipStream_t s) {
+    if (full && a.nk0 == 2) return launch_step3_t<2, true>(a, grid, s);
+    if (full && a.nk0 == 3) return launch_step3_t<3, true>(a, grid, s);
+    return launch_step3_t<s3::NK0MAX, false>(a, grid, s);
 }
 
 hipError_t marf_launch_pack3(const float* params, void* prog, float* bias_out, int* kmap, const Pack2Args& a,
