@@ -70,6 +70,11 @@ MARF_DEV void s3_st16(void* dst, uint4 u) {
     const s3_u32x4 v = {u.x, u.y, u.z, u.w};
     asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
+template <int OFF>
+MARF_DEV void s3_st16o(void* base, uint4 u) {  // 16 B at base + OFF bytes (instruction offset)
+    const s3_u32x4 v = {u.x, u.y, u.z, u.w};
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2\n\ts_nop 1" ::"v"(base), "v"(v), "n"(OFF) : "memory");
+}
 MARF_DEV void s3_st12(void* dst, float a, float b, float c) {
     typedef float f32x3 __attribute__((ext_vector_type(3)));
     f32x3 v = {a, b, c};
@@ -153,6 +158,20 @@ MARF_DEV uint2 s3_bwd_ep(const f32x4& acc, uint32_t mw) {
 
 // ------------------------------------------------------------------ the kernel
 
+// Diagnostic phase timing (MARF_STAMPS builds): wave 0 of each block sums s_memtime deltas per
+// phase category (tools/step2_phases.py --kernel step3 prints them).
+#ifdef MARF_STAMPS
+#define S3T_BEGIN(k) const unsigned long long _t##k = __builtin_amdgcn_s_memtime()
+#define S3T_END(k) tacc[k] += __builtin_amdgcn_s_memtime() - _t##k
+#else
+#define S3T_BEGIN(k) \
+    do {         \
+    } while (0)
+#define S3T_END(k) \
+    do {       \
+    } while (0)
+#endif
+
 // NK0T: layer-0 k-steps (nb + 1 = ceil(L / 8) + 1); FULL: every hidden layer 256 wide.  Both make
 // the row-tile and k-step counts compile-time (no guards, no merges of partly written operand
 // arrays, which cost registers); <NK0MAX, false> is the generic instantiation.
@@ -188,6 +207,9 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
     uint32_t* mkl = reinterpret_cast<uint32_t*>(wpriv + W_MASK);  // [layer][word][lane]
     float* wla = reinterpret_cast<float*>(wpriv + W_WLA);      // [3][Kl] dW_last of the wave
     float* dmy = a.dummy + (((size_t)blockIdx.x * NW + wave) * 64 + lane) * 16;  // 64-B store sink per lane
+#ifdef MARF_STAMPS
+    unsigned long long tacc[16] = {};
+#endif
 
     // ---- constants into LDS (plain loads before the ring starts)
     for (int e = threadIdx.x; e < a.nbias; e += NW * 64) bias_l[e] = a.bias[e];
@@ -221,15 +243,21 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                  __builtin_amdgcn_readfirstlane(base + 4 * TPX * 4));
     };
 
-    // ---- the weight ring: stage c of this block is program stage c mod nS, in slot c mod 3
-    int c_stage = 0, dma_stage = 0;
+    // ---- the weight ring: stage c of this block is program stage c mod nS, in slot c mod 3 (the
+    //      counters wrap instead of dividing)
+    int c_slot = 0;                   // slot of the next stage_begin
+    int dma_stage = 0, dma_ps = 0, dma_slot = 0;  // next DMA: block stage, program stage, slot
     unsigned dma_m0 = 0;
     const char* dma_va = nullptr;
+    const char* const prog_w = a.prog + wave * PER_DMA * 1024 + lane * 16;
+    const unsigned lds_w = lds0 + wave * PER_DMA * 1024;
     auto dma_arm = [&]() {
-        const int ps = dma_stage < total ? dma_stage % nS : 0;  // past the end: refill from stage 0 (never read)
-        dma_m0 = __builtin_amdgcn_readfirstlane(lds0 + (dma_stage % NSLOT) * SLOT + wave * PER_DMA * 1024);
-        dma_va = a.prog + (size_t)ps * SLOT + wave * PER_DMA * 1024 + lane * 16;
+        const int ps = dma_stage < total ? dma_ps : 0;  // past the end: refill from stage 0 (never read)
+        dma_m0 = __builtin_amdgcn_readfirstlane(lds_w + dma_slot * SLOT);
+        dma_va = prog_w + (size_t)ps * SLOT;
         ++dma_stage;
+        dma_ps = dma_ps + 1 == nS ? 0 : dma_ps + 1;
+        dma_slot = dma_slot == NSLOT - 1 ? 0 : dma_slot + 1;
     };
     auto dma_piece = [&](auto jc) {
         constexpr int j = decltype(jc)::value;
@@ -256,16 +284,22 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         else s3_wait_vm<PER_DMA>();
     };
     auto stage_begin = [&]() -> const char* {
+        S3T_BEGIN(0);
         wait_ring();
         st_prev = st_cur;
         st_cur = 0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        S3T_END(0);
+        S3T_BEGIN(1);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        S3T_END(1);
+        S3T_BEGIN(2);
         dma_arm();
         dma_burst();
-        const char* slot = smem + (c_stage % NSLOT) * SLOT;
-        ++c_stage;
+        S3T_END(2);
+        const char* slot = smem + c_slot * SLOT;
+        c_slot = c_slot == NSLOT - 1 ? 0 : c_slot + 1;
         return slot;
     };
 
@@ -341,17 +375,22 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
     // a packed k-step (x, y: features 32 s + 4 g + 0..3 of the lane's pixel; z, w: 32 s + 16 + 4 g + 0..3)
     // into a natural-order [S][ld] bf16 row: one v_permlane16_swap per dword pair puts features
     // 32 s + 16 (g & 1) + 8 (g >> 1) + 0..7 in every lane: one 16-B store
-    auto store_ks = [&](u16* row, int s, const uint4& u) {
+    //  (row = the lane's row base + 16 (g & 1) + 8 (g >> 1) elements; k-step S at instruction offset 64 S)
+    auto store_ks = [&](u16* row, auto sc, const uint4& u) {
+        constexpr int S = decltype(sc)::value;
         const auto xz = __builtin_amdgcn_permlane16_swap(u.x, u.z, false, false);
         const auto yw = __builtin_amdgcn_permlane16_swap(u.y, u.w, false, false);
-        s3_st16(row + 32 * s + 16 * (grp & 1) + 8 * (grp >> 1), make_uint4(xz[0], yw[0], xz[1], yw[1]));
+        s3_st16o<64 * S>(row, make_uint4(xz[0], yw[0], xz[1], yw[1]));
         st_cur += 1;
     };
+    const int colg = 16 * (grp & 1) + 8 * (grp >> 1);
 
     S3Frag Bh[NKH], Bl[NKH], Oh[NKH], Ol[NKH];
     const float pi_f = 3.14159265358979323846f;
 
+    S3T_BEGIN(15);
     for (int ti = 0; ti < my_tiles; ++ti) {
+        S3T_BEGIN(3);
         const int tile = tbase + ti * (int)gridDim.x;
         const int pb = ti & 1;
         const int b = tile / tpp;
@@ -438,7 +477,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         auto fwd_layer = [&](int l, const S3Frag* BH, const S3Frag* BL, int nk, auto nk_tag, int r0) {
             const int nrt = FULL ? (l == 0 ? NRT : NRT) : ly_int(l, 0);
             const bool save = l + 1 < nl - 1 && !a.fwd_only;
-            u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) : nullptr;
+            u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) + colg : nullptr;
             const int boff = ly_int(l, 2);
             uint32_t* mk = mkl + l * 2 * 64 + lane;
             const char* slot = nullptr;
@@ -454,13 +493,16 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                         if (l == 0 && rt == 0 && ti + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
                     }
                     f32x4 acc = bias_init(boff, rt);
+                    S3T_BEGIN(6);
                     gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt());
+                    S3T_END(6);
+                    S3T_BEGIN(7);
                     const S3Ep e = s3_fwd_ep(acc);
                     mword = (mword << 2) | e.nib;
                     if constexpr (rt & 1) {
                         Oh[rt >> 1].u = make_uint4(ev.h0, ev.h1, e.h0, e.h1);
                         Ol[rt >> 1].u = make_uint4(ev.l0, ev.l1, e.l0, e.l1);
-                        if (save) store_ks(srow, rt >> 1, Oh[rt >> 1].u);
+                        if (save) store_ks(srow, std::integral_constant<int, (rt >> 1)>(), Oh[rt >> 1].u);
                     } else {
                         ev = e;
                     }
@@ -468,6 +510,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                         mk[(rt >> 3) * 64] = mword << (2 * (7 - (rt & 7)));
                         mword = 0;
                     }
+                    S3T_END(7);
                 } else if constexpr ((rt & 1) == 0) {
                     Oh[rt >> 1].u = Ol[rt >> 1].u = make_uint4(0, 0, 0, 0);
                 }
@@ -478,8 +521,14 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                 Bl[k] = Ol[k];
             }
         };
+        S3T_END(3);
+        S3T_BEGIN(4);
         fwd_layer(0, Bh, Bl, nk0, NK0t(), FULL ? R0F : a.r0);
+        S3T_END(4);
+        S3T_BEGIN(5);
         for (int l = 1; l < nl - 1; ++l) fwd_layer(l, Bh, Bl, NKH, NKHt(), 2);
+        S3T_END(5);
+        S3T_BEGIN(8);
 
         // ---- last layer: 3 outputs (rows 0..2 of one tile, lanes 0..15), sigmoid, masked MSE, d rgb
         float g[3] = {0.f, 0.f, 0.f};
@@ -513,8 +562,10 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
             s3_st12(o, yv[0], yv[1], yv[2]);
             st_cur += 1;
         }
+        S3T_END(8);
         if (a.fwd_only) continue;
 
+        S3T_BEGIN(9);
         // g as a split pair: hi = bf16(g), lo = bf16(g - hi)
         float ghi[3], glo[3];
 #pragma unroll
@@ -572,6 +623,8 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
             }
         }
 
+        S3T_END(9);
+        S3T_BEGIN(10);
         // ---- last-layer dgrad: dfeat = W_{n-1}^T g (one k-step per row tile: lanes 0..15 carry
         //      k = [g hi (3), 0, g lo (3), 0]), mask -> dz_{n-1}; one stage holds every row tile
         S3Frag gB;
@@ -588,7 +641,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         }
         auto bwd_pass = [&](int l, int lmask, int nrt, const char* slot_first, bool last) {
             // row tiles of dz: last: every tile from one stage (tile rt at rt KB); else two per stage
-            u16* brow = ly_ptr(l, 1) + myslot * ly_int(l, 4);
+            u16* brow = ly_ptr(l, 1) + myslot * ly_int(l, 4) + colg;
             const uint32_t* mk = mkl + lmask * 2 * 64 + lane;
             const char* slot = slot_first;
             uint32_t mw = 0, hv0 = 0, hv1 = 0;
@@ -598,19 +651,25 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                     if constexpr ((rt & 7) == 0) mw = mk[(rt >> 3) * 64];
                     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
                     if (last) {
+                        S3T_BEGIN(11);
                         gemm(acc, slot + rt * 1024, &gB, &gB, 1, NK1t(), MBt());
+                        S3T_END(11);
                     } else {
                         if constexpr ((rt & 1) == 0) slot = stage_begin();
+                        S3T_BEGIN(11);
                         gemm(acc, slot + (rt & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt());
+                        S3T_END(11);
                     }
+                    S3T_BEGIN(12);
                     const uint2 hw = s3_bwd_ep<2 * (7 - (rt & 7))>(acc, mw);
                     if constexpr (rt & 1) {
                         Oh[rt >> 1].u = make_uint4(hv0, hv1, hw.x, hw.y);
-                        store_ks(brow, rt >> 1, Oh[rt >> 1].u);
+                        store_ks(brow, std::integral_constant<int, (rt >> 1)>(), Oh[rt >> 1].u);
                     } else {
                         hv0 = hw.x;
                         hv1 = hw.y;
                     }
+                    S3T_END(12);
                 } else if constexpr ((rt & 1) == 0) {
                     Oh[rt >> 1].u = make_uint4(0, 0, 0, 0);
                 }
@@ -623,6 +682,8 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
             bwd_pass(nl - 1, nl - 2, FULL ? NRT : ly_int(nl - 1, 1), slot, true);
         }
         for (int l = nl - 2; l >= 1; --l) bwd_pass(l, l - 1, FULL ? NRT : ly_int(l, 1), nullptr, false);
+        S3T_END(10);
+        S3T_BEGIN(13);
 
         // ---- layer-0 dgrad + posenc adjoint: row tile t, register r of lane group G holds band
         //      4 t + r of coordinate G >> 1, the sin slot for even G, the cos slot for odd G (the raw
@@ -656,6 +717,8 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                 }
             });
         }
+        S3T_END(13);
+        S3T_BEGIN(14);
         // ---- (u, v) = X[:2] / (X[2] + 1e-8) backward, the bmm backward -> dH partial of the wave
         {
             const float tot = dc + __shfl_xor(dc, 16, 64);  // groups 0 + 1: du, 2 + 3: dv
@@ -689,7 +752,13 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
             s3_st4(lane < 9 ? (void*)(a.dH_partial + (size_t)(slot0 / PX) * 9 + lane) : (void*)dmy, mine);
             st_cur += 1;
         }
+        S3T_END(14);
     }
+    S3T_END(15);
+#ifdef MARF_STAMPS
+    if (a.stamps && threadIdx.x == 0)
+        for (int k = 0; k < 16; ++k) a.stamps[(size_t)blockIdx.x * 16 + k] = tacc[k];
+#endif
 
     // ---- per-block partials (fixed order over waves)
     s3_wait_vm<0>();

@@ -13,7 +13,7 @@ while read -r CTRS; do
   [ -z "$CTRS" ] && continue
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $CTRS --kernel-trace --output-format csv -d $OUT/pass$i -o run \
-     --kernel-include-regex "k_mlp|k_wgrad|k_step2|k_prologue" -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-render $PMC_BENCH_ARGS > $OUT/pass$i.log 2>&1
+     --kernel-include-regex "${PMC_REGEX:-k_mlp|k_wgrad|k_step2|k_step3|k_prologue}" -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-render $PMC_BENCH_ARGS > $OUT/pass$i.log 2>&1
   rc=$?
   echo "pass $i ($CTRS): exit $rc"
   [ $rc -ne 0 ] && { tail -5 $OUT/pass$i.log; break; }

@@ -69,7 +69,7 @@ if "--traffic" in sys.argv:
     for r in rows:
         k = r["kernel"]
         name = None
-        if k.startswith("k_mlp_step") or k.startswith("k_step2"):
+        if k.startswith("k_mlp_step") or k.startswith("k_step2") or k.startswith("k_step3"):
             name = "mlp_step"
         elif k.startswith("k_prologue_probe"):
             name = "prologue_probe"

@@ -21,10 +21,19 @@ NAMES = ["stage wait+barrier", "DMA issue", "backward (BWL..BW0)", "dH tail", "p
          "  fwd operand copies (B = O)", "  fwd bias init"]
 
 
+NAMES3 = ["stage vmcnt/lgkmcnt wait", "barrier", "DMA issue", "prologue", "forward layer 0", "forward hidden layers",
+          "  in fwd GEMM bodies", "  fwd epilogue + stores", "last layer + loss", "dW_last",
+          "dgrad (last + hidden)", "  in dgrad GEMM bodies", "  dgrad epilogue + stores", "layer-0 adjoint",
+          "dH tail", "tile loop total"]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16x3")
+    ap.add_argument("--kernel", default="step2", choices=["step2", "step3"],
+                    help="step3: the two-waves-per-SIMD kernel (marf_step3.hip, MARF_STEP3=1)")
     args = ap.parse_args()
+    names, total_col = (NAMES3, 15) if args.kernel == "step3" else (NAMES, 7)
     import marf_hip
     from model import planar
     from util import EasyDict as edict
@@ -47,11 +56,11 @@ def main():
         m.graph.compute_loss(v).rgb.backward()
     torch.cuda.synchronize()
     st = stamps.view(-1, 16).cpu().numpy().astype(np.float64)[:, :16]
-    st = st[st[:, 7] > 0]
-    tiles = 4194304 // (32 * (4 if args.precision == "bf16x3" else 8)) / len(st)
+    st = st[st[:, total_col] > 0]
+    tiles = 4194304 // 128 / len(st)
     mean = st.mean(0) / tiles
-    for n, v in zip(NAMES, mean):
-        print(f"{n:24s} {v:10.0f} cycles/tile  {100 * v / mean[7]:5.1f} %")
+    for n, v in zip(names, mean):
+        print(f"{n:24s} {v:10.0f} cycles/tile  {100 * v / mean[total_col]:5.1f} %")
 
 
 if __name__ == "__main__":
