@@ -687,11 +687,15 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
 
         // ---- layer-0 dgrad + posenc adjoint: row tile t, register r of lane group G holds band
         //      4 t + r of coordinate G >> 1, the sin slot for even G, the cos slot for odd G (the raw
-        //      coordinates: tile 2 nb, register 0 of groups 0 (u) and 2 (v))
+        //      coordinates: tile 2 nb, register 0 of groups 0 (u) and 2 (v)).  One v_permlane16_swap
+        //      gives each lane its partner group's slot of the same band, so every lane forms the
+        //      band's term as k_step2 and torch's autograd of sin / cos do, (g_sin cos - g_cos sin)
+        //      2^k pi, accumulated over the bands in increasing k, then the raw coordinate
         float dc = 0.f;
         {
             const int nta = FULL ? NTA : a.nta;
             const float cd = (grp >> 1) ? v : u;
+            const bool sinl = (grp & 1) == 0;
             const char* slot = nullptr;
             s3_sfor<NTA>([&](auto tc) {
                 constexpr int t = decltype(tc)::value;
@@ -703,16 +707,23 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int k = 4 * t + r;
+                            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[r]), __float_as_uint(acc[r]),
+                                                                            false, false);
+                            const float other = __uint_as_float(sinl ? sw[1] : sw[0]);
                             if (k < L) {
                                 float sn, co;
                                 band_sincos<true>(cd, k, sn, co);
-                                float gv = acc[r];
-                                if (a.c2f_on) gv = gv * c2f_l[k];
-                                dc += ((grp & 1) ? -(gv * sn) : gv * co) * ldexpf(pi_f, k);
+                                float gs = sinl ? acc[r] : other, gc = sinl ? other : acc[r];
+                                if (a.c2f_on) {
+                                    const float w = c2f_l[k];
+                                    gs = gs * w;
+                                    gc = gc * w;
+                                }
+                                dc += (gs * co - gc * sn) * ldexpf(pi_f, k);
                             }
                         }
                     } else if (t == 2 * nb) {
-                        if ((grp & 1) == 0) dc += acc[0];
+                        dc += acc[0];  // (read from groups 0 and 2 only)
                     }
                 }
             });
@@ -721,8 +732,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         S3T_BEGIN(14);
         // ---- (u, v) = X[:2] / (X[2] + 1e-8) backward, the bmm backward -> dH partial of the wave
         {
-            const float tot = dc + __shfl_xor(dc, 16, 64);  // groups 0 + 1: du, 2 + 3: dv
-            const float du = tot, dv = __shfl(tot, (lane & 15) + 32, 64);
+            const float du = dc, dv = __shfl(dc, (lane & 15) + 32, 64);  // groups 0: du, 2: dv
             float h9[9];
 #pragma unroll
             for (int e = 0; e < 9; ++e) h9[e] = 0.f;
