@@ -262,7 +262,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
     auto dma_piece = [&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const char* va = dma_va;
-        const unsigned m = dma_m0;
+        const unsigned m = __builtin_amdgcn_readfirstlane(dma_m0);  // an SGPR even under pressure
         unsigned keep;  // m0 is reserved to the compiler: saved and restored around the piece
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off offset:%3\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep)
@@ -295,8 +295,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         asm volatile("" ::: "memory");
         S3T_END(1);
         S3T_BEGIN(2);
-        dma_arm();
-        dma_burst();
+        dma_arm();  // the pieces go out beside the stage's first MFMAs (gemm's PC flag) or in a burst
         S3T_END(2);
         const char* slot = smem + c_slot * SLOT;
         c_slot = c_slot == NSLOT - 1 ? 0 : c_slot + 1;
@@ -322,9 +321,14 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
     // one 16-row output tile over NK k-steps (nk live): MODE 1 split forward (hi.hi + hi.lo + lo.hi),
     // MODE 2 split dgrad (hi.B + lo.B).  A fragments of k-step ks at slot + ks KB (hi) and + LO (lo),
     // read two k-steps ahead.
-    auto gemm = [&](f32x4& acc, const char* slot, const S3Frag* Bh, const S3Frag* Bl, int nk, auto nk_tag, auto mode_tag) {
+    // PC: this GEMM is its stage's first -- the stage's DMA pieces go out beside its MFMAs (piece j
+    // after k-step 2 j of an 8-k-step GEMM; after the last k-step of a shorter one), so the MFMAs
+    // start right after the barrier; every store of the stage follows (the ring-wait accounting)
+    auto gemm = [&](f32x4& acc, const char* slot, const S3Frag* Bh, const S3Frag* Bl, int nk, auto nk_tag, auto mode_tag,
+                    auto pc_tag) {
         constexpr int NK = decltype(nk_tag)::value;
         constexpr int MODE = decltype(mode_tag)::value;
+        constexpr bool PC = decltype(pc_tag)::value;
         const bf16x8* ah = reinterpret_cast<const bf16x8*>(slot + lane * 16);
         const bf16x8* al = reinterpret_cast<const bf16x8*>(slot + LO + lane * 16);
         bf16x8 A0[2], A1[2];
@@ -359,9 +363,13 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
             }
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (ks + 2 < NK) A1[u] = al[(ks + 2) * 64];
+            if constexpr (PC && NK == NKH && (ks & 1) == 0) dma_piece(std::integral_constant<int, ks / 2>());
             __builtin_amdgcn_sched_barrier(0);
         });
+        if constexpr (PC && NK != NKH) dma_burst();
     };
+    typedef std::integral_constant<bool, true> PcOn;
+    typedef std::integral_constant<bool, false> PcOff;
     typedef std::integral_constant<int, 1> MFt;
     typedef std::integral_constant<int, 2> MBt;
     typedef std::integral_constant<int, NKH> NKHt;
@@ -494,7 +502,10 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                     }
                     f32x4 acc = bias_init(boff, rt);
                     S3T_BEGIN(6);
-                    gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt());
+                    if (sub == 0)
+                        gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt(), PcOn());
+                    else
+                        gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt(), PcOff());
                     S3T_END(6);
                     S3T_BEGIN(7);
                     const S3Ep e = s3_fwd_ep(acc);
@@ -535,7 +546,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         {
             f32x4 acc = bias_init(ly_int(nl - 1, 2), 0);
             const char* slot = stage_begin();
-            gemm(acc, slot, Bh, Bl, NKH, NKHt(), MFt());
+            gemm(acc, slot, Bh, Bl, NKH, NKHt(), MFt(), PcOn());
             float* o = (a.rgb && valid && grp == 0) ? a.rgb + ((size_t)b * Np + p) * 3 : dmy;
             float yv[3] = {0.f, 0.f, 0.f};
             if (grp == 0) {
@@ -652,12 +663,16 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
                     if (last) {
                         S3T_BEGIN(11);
-                        gemm(acc, slot + rt * 1024, &gB, &gB, 1, NK1t(), MBt());
+                        if constexpr (rt == 0)
+                            gemm(acc, slot + rt * 1024, &gB, &gB, 1, NK1t(), MBt(), PcOn());
+                        else
+                            gemm(acc, slot + rt * 1024, &gB, &gB, 1, NK1t(), MBt(), PcOff());
                         S3T_END(11);
                     } else {
                         if constexpr ((rt & 1) == 0) slot = stage_begin();
                         S3T_BEGIN(11);
-                        gemm(acc, slot + (rt & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt());
+                        gemm(acc, slot + (rt & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt(),
+                             std::integral_constant<bool, (rt & 1) == 0>());
                         S3T_END(11);
                     }
                     S3T_BEGIN(12);
@@ -702,7 +717,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                 if (t < nta) {
                     if constexpr ((t & 1) == 0) slot = stage_begin();
                     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-                    gemm(acc, slot + (t & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt());
+                    gemm(acc, slot + (t & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt(), std::integral_constant<bool, (t & 1) == 0>());
                     if (t < 2 * nb) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
