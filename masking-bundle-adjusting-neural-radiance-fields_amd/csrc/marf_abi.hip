@@ -156,9 +156,9 @@ static void plan_step2_net(marf_net* n) {
     if (n->dtype != MARF_BF16X3 && !step2_env_enabled()) return;
     q.HM = 256;
     q.variant = n->dtype == MARF_BF16X3 ? 1 : 0;
-    if (q.variant == 1) {  // the two-waves-per-SIMD kernel: MARF_STEP3=1 at net creation (in development)
+    if (q.variant == 1) {  // the two-waves-per-SIMD kernel (k_step3) unless MARF_STEP3=0 at net creation
         const char* e = getenv("MARF_STEP3");
-        if (e && e[0] == '1') {
+        if (!(e && e[0] == '0')) {
             plan_step3_net(n);
             return;
         }
