@@ -19,5 +19,5 @@ b() {  # b <name> [env...]
   python -c "import json; d=json.loads(open('$OUT/bench_$n.json').read().strip().splitlines()[-1]); print('render px/s', d['config']['render_pixels_per_s'])"
 }
 b s3 MARF_STEP3=1
-b s2
+b s2 MARF_STEP3=0
 exit $RC
