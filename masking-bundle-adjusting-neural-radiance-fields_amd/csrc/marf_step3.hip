@@ -79,11 +79,7 @@ MARF_DEV void s3_st16o(void* base, uint4 u) {  // 16 B at base + OFF bytes (inst
     return;
 #endif
     const s3_u32x4 v = {u.x, u.y, u.z, u.w};
-#ifdef S3_NT
-    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 nt\n\ts_nop 1" ::"v"(base), "v"(v), "n"(OFF) : "memory");
-#else
     asm volatile("global_store_dwordx4 %0, %1, off offset:%2\n\ts_nop 1" ::"v"(base), "v"(v), "n"(OFF) : "memory");
-#endif
 }
 MARF_DEV void s3_st12(void* dst, float a, float b, float c) {
     typedef float f32x3 __attribute__((ext_vector_type(3)));
@@ -258,7 +254,6 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
     int c_slot = 0;                   // slot of the next stage_begin
     int dma_stage = 0, dma_ps = 0, dma_slot = 0;  // next DMA: block stage, program stage, slot
     unsigned dma_m0 = 0;
-    int dma_ps_cur = 0;
     const char* dma_va = nullptr;
     const char* const prog_w = a.prog + wave * PER_DMA * 1024 + lane * 16;
     const unsigned lds_w = lds0 + wave * PER_DMA * 1024;
@@ -266,7 +261,6 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         const int ps = dma_stage < total ? dma_ps : 0;  // past the end: refill from stage 0 (never read)
         dma_m0 = __builtin_amdgcn_readfirstlane(lds_w + dma_slot * SLOT);
         dma_va = prog_w + (size_t)ps * SLOT;
-        dma_ps_cur = ps;
         ++dma_stage;
         dma_ps = dma_ps + 1 == nS ? 0 : dma_ps + 1;
         dma_slot = dma_slot == NSLOT - 1 ? 0 : dma_slot + 1;
@@ -276,26 +270,13 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
 #ifdef S3_AB_NODMA  // timing-only A/B builds (wrong results): no weight DMA
         return;
 #endif
+        const char* va = dma_va;
         const unsigned m = __builtin_amdgcn_readfirstlane(dma_m0);  // an SGPR even under pressure
         unsigned keep;  // m0 is reserved to the compiler: saved and restored around the piece
-#ifdef S3_SADDR
-        // uniform base in an SGPR pair + the lane's 32-bit offset
-        const unsigned voff = (threadIdx.x & 63) * 16;
-        const uint64_t sb = (uint64_t)(uintptr_t)a.prog + (uint64_t)(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * PER_DMA * 1024) +
-                            (uint64_t)dma_ps_cur * SLOT;
-        const uint64_t sbu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb)) |
-                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32)) << 32);
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %4 offset:%3\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(voff), "s"(m), "n"(j * 1024), "s"(sbu)
-                     : "memory");
-#else
-        const char* va = dma_va;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off offset:%3\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep)
                      : "v"(va), "s"(m), "n"(j * 1024)
                      : "memory");
-#endif
     };
     auto dma_burst = [&]() { s3_sfor<PER_DMA>([&](auto jc) { dma_piece(jc); }); };
     // The DMA of stage c was issued right after the barrier of stage c - 2; younger than it are the
@@ -361,7 +342,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                     auto pc_tag) {
         constexpr int NK = decltype(nk_tag)::value;
         constexpr int MODE = decltype(mode_tag)::value;
-        constexpr int PC = decltype(pc_tag)::value;
+        constexpr bool PC = decltype(pc_tag)::value;
         const bf16x8* ah = reinterpret_cast<const bf16x8*>(slot + lane * 16);
         const bf16x8* al = reinterpret_cast<const bf16x8*>(slot + LO + lane * 16);
         bf16x8 A0[2], A1[2];
@@ -374,9 +355,6 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         // sched_barrier pins the order: left alone the scheduler sinks each LDS read to right before
         // its MFMA (an lgkmcnt(0) wait per MFMA) to save the ring's registers
         __builtin_amdgcn_sched_barrier(0);
-#ifdef S3_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
         s3_sfor<NK>([&](auto ksc) {
             constexpr int ks = decltype(ksc)::value;
             constexpr int u = ks & 1;
@@ -399,70 +377,13 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
             }
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (ks + 2 < NK) A1[u] = al[(ks + 2) * 64];
-            if constexpr (PC == 1 && NK == NKH && (ks & 1) == 0) dma_piece(std::integral_constant<int, ks / 2>());
-            if constexpr (PC >= 2 && NK == NKH && (ks & 3) == 0) dma_piece(std::integral_constant<int, 2 * (PC - 2) + ks / 4>());
+            if constexpr (PC && NK == NKH && (ks & 1) == 0) dma_piece(std::integral_constant<int, ks / 2>());
             __builtin_amdgcn_sched_barrier(0);
         });
-        if constexpr (PC == 1 && NK != NKH) dma_burst();
-#ifdef S3_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
+        if constexpr (PC && NK != NKH) dma_burst();
     };
-    // the two row tiles of a stage as one 16-k-step stream (row tile 2s + 1's A fragments follow
-    // 2s's in the slot, so the 2-deep A ring runs on across the boundary), with the first tile's
-    // epilogue spread over the second tile's MFMA gaps: ep(piece) after its k-step piece (0..7)
-    auto gemm2 = [&](f32x4& acc0, f32x4& acc1, const char* slot, const S3Frag* Bh, const S3Frag* Bl, auto mode_tag,
-                     auto pc_tag, auto&& ep) {
-        constexpr int MODE = decltype(mode_tag)::value;
-        constexpr int PC = decltype(pc_tag)::value;
-        const bf16x8* ah = reinterpret_cast<const bf16x8*>(slot + lane * 16);
-        const bf16x8* al = reinterpret_cast<const bf16x8*>(slot + LO + lane * 16);
-        bf16x8 A0[2], A1[2];
-        A0[0] = ah[0];
-        A1[0] = al[0];
-        A0[1] = ah[64];
-        A1[1] = al[64];
-        __builtin_amdgcn_sched_barrier(0);
-        s3_sfor<2 * NKH>([&](auto kc) {
-            constexpr int kk = decltype(kc)::value;
-            constexpr int ks = kk % NKH;
-            constexpr int u = kk & 1;
-            f32x4& acc = kk < NKH ? acc0 : acc1;
-            if constexpr (MODE == 1) {
-                mf(acc, A0[u], Bh[ks].f);
-                mf(acc, A0[u], Bl[ks].f);
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (kk + 2 < 2 * NKH) A0[u] = ah[(kk + 2) * 64];
-                mf(acc, A1[u], Bh[ks].f);
-            } else {
-                mf(acc, A0[u], Bh[ks].f);
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (kk + 2 < 2 * NKH) A0[u] = ah[(kk + 2) * 64];
-                mf(acc, A1[u], Bh[ks].f);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (kk + 2 < 2 * NKH) A1[u] = al[(kk + 2) * 64];
-            if constexpr (PC == 1 && kk < NKH && (kk & 1) == 0) dma_piece(std::integral_constant<int, kk / 2>());
-            if constexpr (kk >= NKH) ep(std::integral_constant<int, kk - NKH>());
-            __builtin_amdgcn_sched_barrier(0);
-        });
-    };
-    typedef std::integral_constant<int, 1> PcOn;
-    typedef std::integral_constant<int, 0> PcOff;
-    // the stage's pieces split over its two GEMMs of 8 k-steps (pieces 0, 1 beside the first, 2, 3
-    // beside the second), or all four beside the first
-    // (FULL only: there every such stage has both GEMMs; ONE: the stage's second GEMM is absent)
-#ifdef S3_SPREAD
-    constexpr bool spread = FULL;
-#else
-    constexpr bool spread = false;
-#endif
-    auto pc_of = [&](auto rtc, auto one) {  // PC mode of the GEMM of row tile rt (two per stage)
-        constexpr int rt = decltype(rtc)::value;
-        constexpr bool sp = spread && !decltype(one)::value;
-        return std::integral_constant<int, sp ? ((rt & 1) == 0 ? 2 : 3) : ((rt & 1) == 0 ? 1 : 0)>();
-    };
-    typedef std::integral_constant<bool, false> Two;
+    typedef std::integral_constant<bool, true> PcOn;
+    typedef std::integral_constant<bool, false> PcOff;
     typedef std::integral_constant<int, 1> MFt;
     typedef std::integral_constant<int, 2> MBt;
     typedef std::integral_constant<int, NKH> NKHt;
@@ -485,62 +406,6 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         st_cur += 1;
     };
     const int colg = 16 * (grp & 1) + 8 * (grp >> 1);
-
-    // ---- ping-pong sections (FULL nets: the hidden forward layers, the hidden dgrad layers).  The
-    //      block's two halves -- waves 0-3 and 4-7, one of each on every SIMD -- run the same per-row-
-    //      tile op sequence G(0) E(0) G(1) E(1) ..., half 1 one op behind half 0, with one s_barrier
-    //      per op: in every segment one wave of a SIMD issues a GEMM's MFMAs while its partner does the
-    //      epilogue, the stores and the DMA pieces (G = the row tile's GEMM, E = its epilogue + the
-    //      stage's DMA pieces + the pair's store).  Stage i (row tiles 2i, 2i + 1, one ring slot) is
-    //      read in segments 4i .. 4i + 3; its E ops issue the pieces of stage i + 2 into the slot of
-    //      stage i - 1 (last read in segment 4i - 1); each wave waits for its own pieces of stage i + 1
-    //      before the barrier that ends segment 4i + 3 (counted: pp_ops VMEM ops issued in the section,
-    //      pp_mA / pp_mB = pp_ops right after the last piece of stage i + 1 / i + 2).
-    const bool h1 = wave >= NW / 2;
-    int pp_ops = 0, pp_mA = -1, pp_mB = -1;
-    auto pp_barrier = [&]() {
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-    auto pp_wait = [&]() {
-        if (pp_mA < 0) return;  // pieces issued before the section (the entry waited for them)
-        const int k = pp_ops - pp_mA;
-        if (k >= 6) s3_wait_vm<6>();
-        else if (k >= 4) s3_wait_vm<4>();
-        else if (k >= 2) s3_wait_vm<2>();
-        else if (k >= 1) s3_wait_vm<1>();
-        else s3_wait_vm<0>();
-    };
-    auto pp_enter = [&]() {
-        s3_wait_vm<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        pp_barrier();
-        pp_ops = 0;
-        pp_mA = pp_mB = -1;
-    };
-    auto pp_exit = [&]() {  // everything landed: the in-phase ring accounting starts from zero
-        s3_wait_vm<0>();
-        st_cur = st_prev = 0;
-    };
-    auto pp_slot = [&]() -> const char* {
-        const char* sl = smem + c_slot * SLOT;
-        c_slot = c_slot == NSLOT - 1 ? 0 : c_slot + 1;
-        pp_mA = pp_mB;
-        return sl;
-    };
-    auto pp_dma = [&](auto oddc) {  // E of an even row tile: arm + pieces 0, 1; odd: pieces 2, 3
-        if constexpr (!decltype(oddc)::value) {
-            dma_arm();
-            dma_piece(std::integral_constant<int, 0>());
-            dma_piece(std::integral_constant<int, 1>());
-            pp_ops += 2;
-        } else {
-            dma_piece(std::integral_constant<int, 2>());
-            dma_piece(std::integral_constant<int, 3>());
-            pp_ops += 2;
-            pp_mB = pp_ops;
-        }
-    };
 
     S3Frag Bh[NKH], Bl[NKH], Oh[NKH], Ol[NKH];
     const float pi_f = 3.14159265358979323846f;
@@ -640,43 +505,6 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
             const char* slot = nullptr;
             uint32_t mword = 0;
             S3Ep ev;
-#ifdef S3_PAIR
-            if constexpr (FULL && decltype(nk_tag)::value == NKH) {
-                s3_sfor<NRT / 2>([&](auto sc) {
-                    constexpr int S = decltype(sc)::value;
-                    slot = stage_begin();
-                    f32x4 acc0 = bias_init(boff, 2 * S), acc1 = bias_init(boff, 2 * S + 1);
-                    float x[4];
-                    gemm2(acc0, acc1, slot, BH, BL, MFt(), PcOn(), [&](auto pc) {
-                        constexpr int P = decltype(pc)::value;  // row tile 2S's epilogue in pieces
-                        if constexpr (P == 1) {
-                            x[0] = s3_relu(acc0[0]);
-                            x[1] = s3_relu(acc0[1]);
-                            ev.h0 = s3_pk(x[0], x[1]);
-                        } else if constexpr (P == 2) {
-                            x[2] = s3_relu(acc0[2]);
-                            x[3] = s3_relu(acc0[3]);
-                            ev.h1 = s3_pk(x[2], x[3]);
-                        } else if constexpr (P == 3) {
-                            ev.l0 = s3_pk(x[0] - s3_lo16(ev.h0), x[1] - s3_hi16(ev.h0));
-                        } else if constexpr (P == 4) {
-                            ev.l1 = s3_pk(x[2] - s3_lo16(ev.h1), x[3] - s3_hi16(ev.h1));
-                        } else if constexpr (P == 5) {
-                            ev.nib = (s3_nz_pair(ev.h1) << 1) | s3_nz_pair(ev.h0);
-                        }
-                    });
-                    const S3Ep e = s3_fwd_ep(acc1);
-                    mword = (mword << 4) | (ev.nib << 2) | e.nib;
-                    Oh[S].u = make_uint4(ev.h0, ev.h1, e.h0, e.h1);
-                    Ol[S].u = make_uint4(ev.l0, ev.l1, e.l0, e.l1);
-                    if (save) store_ks(srow, sc, Oh[S].u);
-                    if constexpr ((S & 3) == 3) {  // the mask word of row tiles 8 (S >> 2) .. 2 S + 1
-                        mk[(S >> 2) * 64] = mword;
-                        mword = 0;
-                    }
-                });
-            } else
-#endif
             s3_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;
                 if (rt < nrt) {
@@ -688,18 +516,16 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                     }
                     f32x4 acc = bias_init(boff, rt);
                     S3T_BEGIN(6);
-                    constexpr bool hid = decltype(nk_tag)::value == NKH;  // hidden: two row tiles per stage
-                    if constexpr (hid) {
-                        gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt(), pc_of(rtc, Two()));
-                    } else {
-                        if (sub == 0)
-                            gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt(), PcOn());
-                        else
-                            gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt(), PcOff());
-                    }
+                    if (sub == 0)
+                        gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt(), PcOn());
+                    else
+                        gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt(), PcOff());
                     S3T_END(6);
                     S3T_BEGIN(7);
                     const S3Ep e = s3_fwd_ep(acc);
+                    // the lo words computed here, not deferred to the layer's end, where the compiler
+                    // would keep the 64 fp32 values alive (26 registers)
+                    asm volatile("" ::"v"(e.l0), "v"(e.l1));
                     mword = (mword << 2) | e.nib;
                     if constexpr (rt & 1) {
                         Oh[rt >> 1].u = make_uint4(ev.h0, ev.h1, e.h0, e.h1);
@@ -723,90 +549,12 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                 Bl[k] = Ol[k];
             }
         };
-        // the hidden forward layers 1 .. nl - 2 as one ping-pong section (FULL: 16 row tiles each)
-        auto pp_fwd = [&]() {
-            const char* slot = nullptr;
-            f32x4 acc = {};
-            S3Ep ev = {};
-            uint32_t mword = 0;
-            auto E = [&](auto rtc, u16* srow, uint32_t* mk, bool save) {
-                constexpr int rt = decltype(rtc)::value;
-                const S3Ep e = s3_fwd_ep(acc);
-                mword = (mword << 2) | e.nib;
-                if constexpr (rt & 1) {
-                    Oh[rt >> 1].u = make_uint4(ev.h0, ev.h1, e.h0, e.h1);
-                    Ol[rt >> 1].u = make_uint4(ev.l0, ev.l1, e.l0, e.l1);
-                } else {
-                    ev = e;
-                }
-                if constexpr ((rt & 7) == 7) {  // the mask word of row tiles rt - 7 .. rt
-                    mk[(rt >> 3) * 64] = mword;
-                    mword = 0;
-                }
-                pp_dma(std::integral_constant<bool, (rt & 1) == 1>());
-                if constexpr (rt & 1) {
-                    if (save) {
-                        store_ks(srow, std::integral_constant<int, (rt >> 1)>(), Oh[rt >> 1].u);
-                        pp_ops += 1;
-                    }
-                }
-                if constexpr (rt == NRT - 1) {
-#pragma unroll
-                    for (int k = 0; k < NKH; ++k) {
-                        Bh[k] = Oh[k];
-                        Bl[k] = Ol[k];
-                    }
-                }
-            };
-            u16* srow_p = nullptr;
-            uint32_t* mk_p = nullptr;
-            bool save_p = false;
-            pp_enter();
-            for (int l = 1; l < nl - 1; ++l) {
-                const bool save = l + 1 < nl - 1 && !a.fwd_only;
-                u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) + colg : nullptr;
-                const int boff = ly_int(l, 2);
-                uint32_t* mk = mkl + l * 2 * 64 + lane;
-                const bool prev = l > 1;
-                s3_sfor<NRT>([&](auto rtc) {
-                    constexpr int rt = decltype(rtc)::value;
-                    if (h1) {
-                        if constexpr (rt > 0) E(std::integral_constant<int, rt - 1>(), srow, mk, save);
-                        else if (prev) E(std::integral_constant<int, NRT - 1>(), srow_p, mk_p, save_p);
-                        pp_barrier();
-                    }
-                    if constexpr ((rt & 1) == 0) slot = pp_slot();
-                    acc = bias_init(boff, rt);
-                    gemm(acc, slot + (rt & 1) * NKH * 1024, Bh, Bl, NKH, NKHt(), MFt(), PcOff());
-                    if constexpr (rt & 1) {
-                        if (h1) pp_wait();
-                    }
-                    pp_barrier();
-                    if (!h1) {
-                        E(rtc, srow, mk, save);
-                        if constexpr (rt & 1) pp_wait();
-                        pp_barrier();
-                    }
-                });
-                srow_p = srow;
-                mk_p = mk;
-                save_p = save;
-            }
-            if (h1) E(std::integral_constant<int, NRT - 1>(), srow_p, mk_p, save_p);
-            pp_barrier();
-            pp_exit();
-        };
         S3T_END(3);
         S3T_BEGIN(4);
         fwd_layer(0, Bh, Bl, nk0, NK0t(), FULL ? R0F : a.r0);
         S3T_END(4);
         S3T_BEGIN(5);
-#ifdef S3_PP
-        if constexpr (FULL) {
-            if (nl > 2) pp_fwd();
-        } else
-#endif
-            for (int l = 1; l < nl - 1; ++l) fwd_layer(l, Bh, Bl, NKH, NKHt(), 2);
+        for (int l = 1; l < nl - 1; ++l) fwd_layer(l, Bh, Bl, NKH, NKHt(), 2);
         S3T_END(5);
         S3T_BEGIN(8);
 
@@ -925,35 +673,6 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
             const uint32_t* mk = mkl + lmask * 2 * 64 + lane;
             const char* slot = slot_first;
             uint32_t mw = 0, hv0 = 0, hv1 = 0;
-#ifdef S3_PAIR
-            if constexpr (FULL) {
-                if (!last) {
-                    s3_sfor<NRT / 2>([&](auto sc) {
-                        constexpr int S = decltype(sc)::value;
-                        constexpr int SH0 = 2 * (7 - ((2 * S) & 7)), SH1 = 2 * (7 - ((2 * S + 1) & 7));
-                        if constexpr ((S & 3) == 0) mw = mk[(S >> 2) * 64];
-                        slot = stage_begin();
-                        f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = (f32x4){0.f, 0.f, 0.f, 0.f};
-                        gemm2(acc0, acc1, slot, Bh, Bh, MBt(), PcOn(), [&](auto pc) {
-                            constexpr int P = decltype(pc)::value;  // row tile 2S's epilogue in two pieces
-                            if constexpr (P == 1) {
-                                const int m0 = __builtin_amdgcn_sbfe((int)mw, SH0, 1), m1 = __builtin_amdgcn_sbfe((int)mw, SH0 + 16, 1);
-                                hv0 = s3_pk(__int_as_float(__float_as_int(acc0[0]) & m0), __int_as_float(__float_as_int(acc0[1]) & m1));
-                            } else if constexpr (P == 2) {
-                                const int m2 = __builtin_amdgcn_sbfe((int)mw, SH0 + 1, 1), m3 = __builtin_amdgcn_sbfe((int)mw, SH0 + 17, 1);
-                                hv1 = s3_pk(__int_as_float(__float_as_int(acc0[2]) & m2), __int_as_float(__float_as_int(acc0[3]) & m3));
-                            }
-                        });
-                        const uint2 hw = s3_bwd_ep<SH1>(acc1, mw);
-                        Oh[S].u = make_uint4(hv0, hv1, hw.x, hw.y);
-                        store_ks(brow, sc, Oh[S].u);
-                    });
-#pragma unroll
-                    for (int k = 0; k < NKH; ++k) Bh[k] = Oh[k];
-                    return;
-                }
-            }
-#endif
             s3_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;
                 if (rt < nrt) {
@@ -969,7 +688,8 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                     } else {
                         if constexpr ((rt & 1) == 0) slot = stage_begin();
                         S3T_BEGIN(11);
-                        gemm(acc, slot + (rt & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt(), pc_of(rtc, Two()));
+                        gemm(acc, slot + (rt & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt(),
+                             std::integral_constant<bool, (rt & 1) == 0>());
                         S3T_END(11);
                     }
                     S3T_BEGIN(12);
@@ -989,75 +709,11 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
 #pragma unroll
             for (int k = 0; k < NKH; ++k) Bh[k] = Oh[k];
         };
-        // the hidden dgrad layers nl - 2 .. 1 as one ping-pong section (FULL: 16 row tiles each)
-        auto pp_bwd = [&]() {
-            const char* slot = nullptr;
-            f32x4 acc = {};
-            uint32_t mw = 0, hv0 = 0, hv1 = 0;
-            auto E = [&](auto rtc, u16* brow, const uint32_t* mk) {
-                constexpr int rt = decltype(rtc)::value;
-                if constexpr ((rt & 7) == 0) mw = mk[(rt >> 3) * 64];
-                const uint2 hw = s3_bwd_ep<2 * (7 - (rt & 7))>(acc, mw);
-                if constexpr (rt & 1) {
-                    Oh[rt >> 1].u = make_uint4(hv0, hv1, hw.x, hw.y);
-                } else {
-                    hv0 = hw.x;
-                    hv1 = hw.y;
-                }
-                pp_dma(std::integral_constant<bool, (rt & 1) == 1>());
-                if constexpr (rt & 1) {
-                    store_ks(brow, std::integral_constant<int, (rt >> 1)>(), Oh[rt >> 1].u);
-                    pp_ops += 1;
-                }
-                if constexpr (rt == NRT - 1) {
-#pragma unroll
-                    for (int k = 0; k < NKH; ++k) Bh[k] = Oh[k];
-                }
-            };
-            u16* brow_p = nullptr;
-            const uint32_t* mk_p = nullptr;
-            pp_enter();
-            for (int l = nl - 2; l >= 1; --l) {
-                u16* brow = ly_ptr(l, 1) + myslot * ly_int(l, 4) + colg;
-                const uint32_t* mk = mkl + (l - 1) * 2 * 64 + lane;
-                const bool prev = l < nl - 2;
-                s3_sfor<NRT>([&](auto rtc) {
-                    constexpr int rt = decltype(rtc)::value;
-                    if (h1) {
-                        if constexpr (rt > 0) E(std::integral_constant<int, rt - 1>(), brow, mk);
-                        else if (prev) E(std::integral_constant<int, NRT - 1>(), brow_p, mk_p);
-                        pp_barrier();
-                    }
-                    if constexpr ((rt & 1) == 0) slot = pp_slot();
-                    acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-                    gemm(acc, slot + (rt & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt(), PcOff());
-                    if constexpr (rt & 1) {
-                        if (h1) pp_wait();
-                    }
-                    pp_barrier();
-                    if (!h1) {
-                        E(rtc, brow, mk);
-                        if constexpr (rt & 1) pp_wait();
-                        pp_barrier();
-                    }
-                });
-                brow_p = brow;
-                mk_p = mk;
-            }
-            if (h1) E(std::integral_constant<int, NRT - 1>(), brow_p, mk_p);
-            pp_barrier();
-            pp_exit();
-        };
         {
             const char* slot = stage_begin();
             bwd_pass(nl - 1, nl - 2, FULL ? NRT : ly_int(nl - 1, 1), slot, true);
         }
-#ifdef S3_PP
-        if constexpr (FULL) {
-            if (nl > 2) pp_bwd();
-        } else
-#endif
-            for (int l = nl - 2; l >= 1; --l) bwd_pass(l, l - 1, FULL ? NRT : ly_int(l, 1), nullptr, false);
+        for (int l = nl - 2; l >= 1; --l) bwd_pass(l, l - 1, FULL ? NRT : ly_int(l, 1), nullptr, false);
         S3T_END(10);
         S3T_BEGIN(13);
 
@@ -1078,7 +734,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
                 if (t < nta) {
                     if constexpr ((t & 1) == 0) slot = stage_begin();
                     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-                    gemm(acc, slot + (t & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt(), pc_of(tc, std::integral_constant<bool, (t + 1 >= NTA)>()));
+                    gemm(acc, slot + (t & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt(), std::integral_constant<bool, (t & 1) == 0>());
                     if (t < 2 * nb) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
