@@ -49,6 +49,7 @@ struct Step2NetPlan {
                            // 3: split bf16, two waves per SIMD (marf_step3.hip)
     int NW, NS, HM, MAXR, NMW, slot, nk0, nta, n_stages, nbias, Kl, ldf0;
     int PX, TPX;           // pixels per wave, pixel slots per block tile
+    int nslot;             // weight-ring slots in LDS
     int nk0w;              // k_step2's layer-0 k-steps: feat_0's column layout (weight gradient, kmap)
     int n_fwd;             // the program's forward stages
     int r0, ns0;           // layer-0 row tiles per stage (their k-steps share one slot) and its stages
@@ -105,10 +106,19 @@ static void plan_step3_net(marf_net* n) {
     const int nl = n->n_layers;
     q.variant = 3;
     q.HM = 256;
-    q.NW = 8;
     q.NS = 1;
     q.PX = 16;
-    q.TPX = 128;
+    {
+        // 12 waves (three per SIMD, 2-slot ring) for full-width nets with L <= 16 unless
+        // MARF_S3_NW=8; 8 waves otherwise
+        bool full = n->L >= 1;
+        for (int l = 0; l < nl - 1; ++l) full = full && n->Mp[l] == 256;
+        const char* e = getenv("MARF_S3_NW");
+        const int want = e && e[0] ? atoi(e) : 8;
+        q.NW = marf_step3_nw_ok(full, (n->L + 7) / 8 + 1, want) ? want : 8;
+    }
+    q.TPX = q.NW * q.PX;
+    q.nslot = q.NW == 12 ? 2 : 3;
     q.MAXR = 4;
     q.NMW = 4;
     q.slot = 32768;
@@ -168,6 +178,7 @@ static void plan_step2_net(marf_net* n) {
         if (q.variant == 0 && e && e[0] == '1') q.variant = 2;
     }
     q.NW = q.variant == 0 ? 8 : 4;
+    q.nslot = 3;
     q.NS = q.variant == 1 ? 2 : 1;  // pixel sets per dgrad pass (S2Cfg::NS)
     q.PX = 32;
     q.TPX = 32 * q.NW;
@@ -1054,7 +1065,7 @@ static hipError_t launch_s2(const marf_net* n, const Step2Args& a, int grid, hip
     if (q.variant != 3) return marf_launch_step2(a, q.variant, grid, s);
     bool full = n->L >= 1;  // every hidden layer 256 wide
     for (int l = 0; l < n->n_layers - 1; ++l) full = full && n->Mp[l] == 256;
-    return marf_launch_step3(a, full, grid, s);
+    return marf_launch_step3(a, full, q.NW, grid, s);
 }
 
 static int step2_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
@@ -1114,7 +1125,7 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     a.n_tiles = p.n_tiles;
     // LDS layout
     const int TPX = q.TPX;
-    int off = 3 * q.slot;
+    int off = q.nslot * q.slot;
     a.lds_pro = off;
     off += 2 * (4 * TPX + 64) * 4;
     a.lds_bias = off;

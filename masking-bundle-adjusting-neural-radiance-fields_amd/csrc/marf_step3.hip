@@ -32,22 +32,19 @@
 namespace marf {
 namespace s3 {
 
-constexpr int NW = 8;                         // waves per block: two per SIMD
 constexpr int PX = 16;                        // pixels per wave
-constexpr int TPX = NW * PX;                  // pixel slots per block tile
 constexpr int HM = 256;                       // widest hidden layer
 constexpr int NKH = HM / 32;                  // k-steps (32 k) of a hidden-width operand
 constexpr int NRT = HM / 16;                  // 16-row tiles of a hidden-width output
 constexpr int SLOT = 32768;                   // one ring slot = one program stage
 constexpr int LO = 16384;                     // byte offset of the lo fragments in a slot
-constexpr int PER_DMA = SLOT / (NW * 1024);   // 1 KB DMA pieces per wave and stage
-constexpr int NSLOT = 3;
+constexpr int PER_DMA = 4;                    // 1 KB DMA pieces per DMA wave and stage
 constexpr int NK0MAX = 5;                     // max layer-0 k-steps (L <= 32: 4 band steps + raw)
 constexpr int NML = 4;                        // max ReLU layers (nl <= 5)
 // wave-private LDS: g^T image (256 B), transpose scratch (1 KB), mask words [NML][2][64], dW_last [3][256]
 constexpr int W_GIMG = 0, W_SCR = 256, W_MASK = 1280, W_WLA = W_MASK + NML * 2 * 64 * 4;
 constexpr int WAVE_LDS = W_WLA + 3 * HM * 4;
-static_assert(PER_DMA == 4 && PER_DMA * NW * 1024 == SLOT, "ring geometry");
+static_assert(SLOT % (PER_DMA * 1024) == 0, "ring geometry");
 
 }  // namespace s3
 
@@ -181,9 +178,16 @@ MARF_DEV uint2 s3_bwd_ep(const f32x4& acc, uint32_t mw) {
 // NK0T: layer-0 k-steps (nb + 1 = ceil(L / 8) + 1); FULL: every hidden layer 256 wide.  Both make
 // the row-tile and k-step counts compile-time (no guards, no merges of partly written operand
 // arrays, which cost registers); <NK0MAX, false> is the generic instantiation.
-template <int NK0T, bool FULL>
-__global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
+// NWT: waves per block -- 8 (two per SIMD, 3-slot ring) or 12 (three per SIMD, 2-slot ring: a
+// stage lasts long enough for its successor's DMA; 8 of the 12 waves issue it)
+template <int NK0T, bool FULL, int NWT>
+__global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
     using namespace s3;
+    constexpr int NW = NWT;
+    constexpr int TPX = NW * PX;
+    constexpr int NSLOT = NW == 8 ? 3 : 2;
+    constexpr int NDW = SLOT / (PER_DMA * 1024);  // waves that issue the ring's DMA
+    static_assert(NW == 8 || NW == 12, "waves per block");
     constexpr int NK0 = NK0T;
     constexpr int NTA = 2 * (NK0 - 1) + 1;        // adjoint row tiles (max)
     constexpr int R0F = (16 / NK0) & ~1;           // layer-0 row tiles per stage (FULL)
@@ -255,7 +259,8 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
     int dma_stage = 0, dma_ps = 0, dma_slot = 0;  // next DMA: block stage, program stage, slot
     unsigned dma_m0 = 0;
     const char* dma_va = nullptr;
-    const char* const prog_w = a.prog + wave * PER_DMA * 1024 + lane * 16;
+    const bool dma_wave = NDW == NW || wave < NDW;
+    const char* const prog_w = a.prog + (dma_wave ? wave : 0) * PER_DMA * 1024 + lane * 16;
     const unsigned lds_w = lds0 + wave * PER_DMA * 1024;
     auto dma_arm = [&]() {
         const int ps = dma_stage < total ? dma_ps : 0;  // past the end: refill from stage 0 (never read)
@@ -270,6 +275,7 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
 #ifdef S3_AB_NODMA  // timing-only A/B builds (wrong results): no weight DMA
         return;
 #endif
+        if (!dma_wave) return;
         const char* va = dma_va;
         const unsigned m = __builtin_amdgcn_readfirstlane(dma_m0);  // an SGPR even under pressure
         unsigned keep;  // m0 is reserved to the compiler: saved and restored around the piece
@@ -286,6 +292,19 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
 #ifdef S3_AB_NOWAIT  // timing-only A/B builds (wrong results): no ring wait
         return;
 #endif
+        if constexpr (NSLOT == 2) {  // (every wave: the next tile's inputs are counted in as well)
+            // 2-slot ring: the DMA of stage c went out in stage c - 1; younger: that stage's stores
+            const int y = st_cur;
+            if (y >= 16) s3_wait_vm<16>();
+            else if (y >= 12) s3_wait_vm<12>();
+            else if (y >= 8) s3_wait_vm<8>();
+            else if (y >= 6) s3_wait_vm<6>();
+            else if (y >= 4) s3_wait_vm<4>();
+            else if (y >= 2) s3_wait_vm<2>();
+            else if (y >= 1) s3_wait_vm<1>();
+            else s3_wait_vm<0>();
+            return;
+        }
         const int y = st_prev + st_cur;
         if (y >= 16) s3_wait_vm<PER_DMA + 16>();
         else if (y >= 12) s3_wait_vm<PER_DMA + 12>();
@@ -318,10 +337,10 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
 
     if (my_tiles > 0) {
         issue_pro(tbase, 0);
-        dma_arm();
-        dma_burst();
-        dma_arm();
-        dma_burst();
+        s3_sfor<NSLOT - 1>([&](auto) {
+            dma_arm();
+            dma_burst();
+        });
     }
     s3_wait_vm<0>();
     __syncthreads();
@@ -990,19 +1009,26 @@ __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog
 
 using namespace marf;
 
-template <int NK0T, bool FULL>
+template <int NK0T, bool FULL, int NWT>
 static hipError_t launch_step3_t(const Step2Args& a, int grid, hipStream_t s) {
-    hipError_t e = ensure_dynamic_lds((const void*)k_step3<NK0T, FULL>, (size_t)a.lds_total);
+    hipError_t e = ensure_dynamic_lds((const void*)k_step3<NK0T, FULL, NWT>, (size_t)a.lds_total);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_step3<NK0T, FULL>), dim3(grid), dim3(s3::NW * 64), (size_t)a.lds_total, s, a);
+    hipLaunchKernelGGL((k_step3<NK0T, FULL, NWT>), dim3(grid), dim3(NWT * 64), (size_t)a.lds_total, s, a);
     return hipGetLastError();
 }
 
-// full = every hidden layer 256 wide (the host checks): L <= 8 and L <= 16 get their own code
-hipError_t marf_launch_step3(const Step2Args& a, bool full, int grid, hipStream_t s) {
-    if (full && a.nk0 == 2) return launch_step3_t<2, true>(a, grid, s);
-    if (full && a.nk0 == 3) return launch_step3_t<3, true>(a, grid, s);
-    return launch_step3_t<s3::NK0MAX, false>(a, grid, s);
+// full = every hidden layer 256 wide (the host checks): L <= 8 and L <= 16 get their own code, at 8
+// or 12 waves per block (nw, the plan's); the generic instantiation runs 8
+bool marf_step3_nw_ok(bool full, int nk0, int nw) { return nw == 8 || (nw == 12 && full && (nk0 == 2 || nk0 == 3)); }
+hipError_t marf_launch_step3(const Step2Args& a, bool full, int nw, int grid, hipStream_t s) {
+    if (!marf_step3_nw_ok(full, a.nk0, nw)) return hipErrorInvalidValue;
+    if (nw == 12) {
+        if (a.nk0 == 2) return launch_step3_t<2, true, 12>(a, grid, s);
+        return launch_step3_t<3, true, 12>(a, grid, s);
+    }
+    if (full && a.nk0 == 2) return launch_step3_t<2, true, 8>(a, grid, s);
+    if (full && a.nk0 == 3) return launch_step3_t<3, true, 8>(a, grid, s);
+    return launch_step3_t<s3::NK0MAX, false, 8>(a, grid, s);
 }
 
 hipError_t marf_launch_pack3(const float* params, void* prog, float* bias_out, int* kmap, const Pack2Args& a,
