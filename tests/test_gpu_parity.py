@@ -999,14 +999,19 @@ def test_canvas_geometry_fused_steps_vs_oracle(precision, tmp_path):
         m.graph.warp_param.weight.data[0] = 0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
-def test_c3_two_patch_step_vs_oracle(precision, tmp_path):
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16x3-w12"])
+def test_c3_two_patch_step_vs_oracle(precision, tmp_path, monkeypatch):
     """C3 shape (256x256 crops of a 512 canvas, L=16, 4x256), 2 patches, non-zero warps on both.
+    bf16x3-w12: the opt-in 12-wave k_step3 (MARF_S3_NW=12: 192-pixel tiles, so each 65,536-pixel
+    crop ends in a padded tile of 64 slots).
     rgb <= 1e-5 abs and loss vs oracle.PlanarStep (fp32 <= 1e-6 rel).  Gradients against the
     float64 reference ops: fp32 within 1e-5 relative to their max OR within 2x the reference's own
     fp32 error, whichever is larger (_compare_step); bf16x3 (the bench recipe) within 1e-2 (north_star
     bf16 bound) AND within 2x the reference's own fp32 error (measured: MLP 4.9e-4 vs the
     reference's 4.7e-4; d warp 6.9e-3 vs 5.3e-3 -- a 2 x 65,536-pixel sum that cancels)."""
+    if precision == "bf16x3-w12":
+        monkeypatch.setenv("MARF_S3_NW", "12")
+        precision = "bf16x3"
     m, var, inputs = _synthetic_setup(precision, tmp_path, 2, 256, 16, [256] * 4)
     o = _compare_step(m, var, inputs, precision, 5)
     assert o["rgb"] <= 1e-5
