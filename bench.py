@@ -284,7 +284,9 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t)
     loss_v = float(loss.rgb.detach())
-    assert np.isfinite(loss_v) or os.environ.get("MARF_AB_TIMING_ONLY") == "1", "loss is not finite"
+    timing_only = os.environ.get("MARF_AB_TIMING_ONLY") == "1"  # A/B builds whose results are wrong on purpose
+    assert np.isfinite(loss_v) or timing_only, "loss is not finite"
+    step_kernel = graph.neural_image.engine(dev).net.step_kernel
 
     # ---- forward-only render rate (reported beside the step): Graph.forward without
     #      grad = grid -> warp -> posenc -> MLP -> rgb over the same patches (k_mlp_fwd, no saves)
@@ -364,12 +366,15 @@ def main():
                    "step_tflops_per_gpu": value / world * F / 1e12,
                    "step_frac_of_peak": value / world * F / peak,
                    "loss_rgb_last": loss_v,
+                   "step_kernel": step_kernel,
                    "render_pixels_per_s": render_pps},
         "roofline": roof,
         "prologue": prologue,
         "kernels": per_kernel,
         "kernel_ms_per_step": step_kernel_ms,
     }
+    if timing_only:
+        out["timing_only"] = True  # never a headline: the build under test computes wrong results
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_patches)
     if rank == 0:

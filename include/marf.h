@@ -114,6 +114,9 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
 void marf_net_destroy(marf_net* net);
 long long marf_net_param_count(const marf_net* net);
 size_t marf_net_packed_bytes(const marf_net* net);
+/* Name of the kernel that runs this net's fused training step ("k_step2", "k_step3", "k_mlp_step"),
+ * fixed at net creation (no reference counterpart: measurement and test bookkeeping). */
+const char* marf_net_step_kernel(const marf_net* net);
 /* Pipelined weight gradients of the fused step (no reference counterpart: scheduling only; the
  * reference's loss.all.backward() at model/planar.py:196 computes the same sums).  mode 0 = off
  * (default; env MARF_PIPE at net creation), 1 = on at any size, -1 = on for large steps.  When on,

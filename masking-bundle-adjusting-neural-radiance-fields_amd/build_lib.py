@@ -69,7 +69,7 @@ def _compile(lib_path, extra, verbose):
     import tempfile
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     os.makedirs(os.path.dirname(lib_path), exist_ok=True)
-    tmp = lib_path + ".tmp"
+    tmp = f"{lib_path}.tmp.{os.getpid()}"  # per process: concurrent builders never share a file
     if verbose:
         print("[marf] building", lib_path, flush=True)
     jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))

@@ -108,17 +108,9 @@ static void plan_step3_net(marf_net* n) {
     q.HM = 256;
     q.NS = 1;
     q.PX = 16;
-    {
-        // 12 waves (three per SIMD, 2-slot ring) for full-width nets with L <= 16 unless
-        // MARF_S3_NW=8; 8 waves otherwise
-        bool full = n->L >= 1;
-        for (int l = 0; l < nl - 1; ++l) full = full && n->Mp[l] == 256;
-        const char* e = getenv("MARF_S3_NW");
-        const int want = e && e[0] ? atoi(e) : 8;
-        q.NW = marf_step3_nw_ok(full, (n->L + 7) / 8 + 1, want) ? want : 8;
-    }
+    q.NW = 8;
     q.TPX = q.NW * q.PX;
-    q.nslot = q.NW == 12 ? 2 : 3;
+    q.nslot = 3;
     q.MAXR = 4;
     q.NMW = 4;
     q.slot = 32768;
@@ -166,9 +158,9 @@ static void plan_step2_net(marf_net* n) {
     if (n->dtype != MARF_BF16X3 && !step2_env_enabled()) return;
     q.HM = 256;
     q.variant = n->dtype == MARF_BF16X3 ? 1 : 0;
-    if (q.variant == 1) {  // the two-waves-per-SIMD kernel (k_step3) unless MARF_STEP3=0 at net creation
+    if (q.variant == 1) {  // the two-waves-per-SIMD kernel (k_step3) on request: MARF_STEP3=1 at net creation
         const char* e = getenv("MARF_STEP3");
-        if (!(e && e[0] == '0')) {
+        if (e && e[0] == '1') {
             plan_step3_net(n);
             return;
         }
@@ -516,6 +508,12 @@ int marf_net_set_pipeline(marf_net* net, int mode, int wg_blocks, int piece_tile
 }
 long long marf_net_param_count(const marf_net* net) { return net ? net->param_count : -1; }
 size_t marf_net_packed_bytes(const marf_net* net) { return net ? net->packed_bytes : 0; }
+const char* marf_net_step_kernel(const marf_net* net) {
+    if (!net) return "";
+    if (net->s2.variant == 3) return "k_step3";
+    if (net->s2.variant >= 0) return "k_step2";
+    return "k_mlp_step";
+}
 
 int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, void* stream) {
     if (!net || !d_params || !d_packed) return fail(MARF_ERR_INVALID, "net_pack: NULL argument");

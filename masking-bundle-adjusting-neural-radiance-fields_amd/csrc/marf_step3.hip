@@ -1017,15 +1017,11 @@ static hipError_t launch_step3_t(const Step2Args& a, int grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-// full = every hidden layer 256 wide (the host checks): L <= 8 and L <= 16 get their own code, at 8
-// or 12 waves per block (nw, the plan's); the generic instantiation runs 8
-bool marf_step3_nw_ok(bool full, int nk0, int nw) { return nw == 8 || (nw == 12 && full && (nk0 == 2 || nk0 == 3)); }
+// full = every hidden layer 256 wide (the host checks): L <= 8 and L <= 16 get their own code; the
+// generic instantiation covers the rest.  8 waves per block (two per SIMD).
+bool marf_step3_nw_ok(bool, int, int nw) { return nw == 8; }
 hipError_t marf_launch_step3(const Step2Args& a, bool full, int nw, int grid, hipStream_t s) {
-    if (!marf_step3_nw_ok(full, a.nk0, nw)) return hipErrorInvalidValue;
-    if (nw == 12) {
-        if (a.nk0 == 2) return launch_step3_t<2, true, 12>(a, grid, s);
-        return launch_step3_t<3, true, 12>(a, grid, s);
-    }
+    if (nw != 8) return hipErrorInvalidValue;
     if (full && a.nk0 == 2) return launch_step3_t<2, true, 8>(a, grid, s);
     if (full && a.nk0 == 3) return launch_step3_t<3, true, 8>(a, grid, s);
     return launch_step3_t<s3::NK0MAX, false, 8>(a, grid, s);

@@ -48,6 +48,7 @@ _SIGS = {
     "marf_net_destroy": (None, [_c_vp]),
     "marf_net_param_count": (_c_ll, [_c_vp]),
     "marf_net_packed_bytes": (_c_sz, [_c_vp]),
+    "marf_net_step_kernel": (ctypes.c_char_p, [_c_vp]),
     "marf_net_pack": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_net_set_pipeline": (_c_int, [_c_vp, _c_int, _c_int, _c_int]),
     "marf_saved_bytes": (_c_sz, [_c_vp, ctypes.POINTER(Geometry)]),
@@ -99,7 +100,18 @@ def _ensure_current():
               file=sys.stderr, flush=True)
         return
     try:
-        build_lib.build(force=True, verbose=False)
+        # one builder at a time (torchrun ranks, spawned test workers): the lock is held across the
+        # re-check and the build, so a process that waited finds the fresh library and loads it
+        import fcntl
+        os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+        with open(LIB_PATH + ".lock", "w") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            try:
+                have = build_lib.embedded_hash(LIB_PATH) if os.path.exists(LIB_PATH) else None
+                if have != want:
+                    build_lib.build(force=True, verbose=False)
+            finally:
+                fcntl.flock(lk, fcntl.LOCK_UN)
     except Exception as e:  # pragma: no cover - message path
         raise RuntimeError(f"libmarf.so at {LIB_PATH} is missing or stale and could not be built: {e}") from e
 
@@ -356,6 +368,7 @@ class Net:
         self._h = h
         self.param_count = lib().marf_net_param_count(h)
         self.packed_bytes = lib().marf_net_packed_bytes(h)
+        self.step_kernel = lib().marf_net_step_kernel(h).decode()
 
     @property
     def handle(self):

@@ -815,11 +815,10 @@ def _reference_runs():
     return runs
 
 
-@pytest.mark.parametrize("precision", ["bf16x3", "bf16x3-step2", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
 def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path, monkeypatch):
     """BASELINE config 1/2 end to end: the seed=3 cat_batch3 run for 3000 iterations, for the recipe
-    the bench measures (bf16x3, on the default two-waves-per-SIMD kernel k_step3), for the same
-    recipe on the one-wave kernel k_step2 (bf16x3-step2: MARF_STEP3=0), and for fp32.
+    and kernel the bench measures (bf16x3 on the default step kernel) and for fp32.
 
     PSNR: final within 0.05 dB of the reference's 25.9968 dB (north_star).
     Warps: the north_star's 1e-2 cannot be met against a single reference run by the reference
@@ -829,15 +828,9 @@ def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path, monkeypatch):
     the absolute warps must lie within 3e-2 of the nearest reference run.
 
     The run is chaotic: which basin patch 1's perspective row settles in (26.0 dB or 24.3-25.0 dB)
-    is re-rolled by any change of fp32 rounding order.  The two kernels compute the same recipe in
-    different summation orders (per-step gradient errors against float64 equal, tools/s3_err.py);
-    over the same 40 one-ulp init draws k_step2 lands 18 and k_step3 24 in the 26 dB basin
-    (profiles/r3k_basin/).  k_step2's seed-3 draw lands there and meets the contract; k_step3's
-    seed-3 draw lands in the 24.6 dB basin: recorded as an expected failure of that draw, not
-    hidden, while every run that does reach the 26 dB basin is held to the contract."""
-    if precision == "bf16x3-step2":
-        monkeypatch.setenv("MARF_STEP3", "0")
-        precision = "bf16x3"
+    is re-rolled by any change of fp32 rounding order, so the kernel the bench times must be the
+    kernel whose arithmetic this run pins."""
+    monkeypatch.delenv("MARF_STEP3", raising=False)
     psnr, warps = _run_c1(precision, tmp_path)
     runs = _reference_runs()
     err = warps[1:] - REF_WARPS_3000
@@ -851,9 +844,6 @@ def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path, monkeypatch):
     if os.environ.get("MARF_C1_SEPARATE"):
         p2, w2 = _run_c1(precision, tmp_path, fused=False)
         print(f"{precision} separate kernels: final PSNR {p2[-1]:.4f}; max |warp - fused| {np.abs(w2 - warps).max():.2e}")
-    if precision == "bf16x3" and os.environ.get("MARF_STEP3") != "0" and psnr[-1] < 25.5:
-        pytest.xfail(f"k_step3's seed-3 draw ends in the {psnr[-1]:.2f} dB basin (chaotic basin selection; "
-                     "same-draw basin statistics equal to k_step2's, profiles/r3k_basin/)")
     assert abs(psnr[-1] - REF_PSNR_3000) <= 0.05, psnr[-10:]
     assert np.abs(resid).max() <= 1e-2, resid
     assert nearest <= 3e-2, nearest
@@ -999,18 +989,17 @@ def test_canvas_geometry_fused_steps_vs_oracle(precision, tmp_path):
         m.graph.warp_param.weight.data[0] = 0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16x3-w12"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16x3-step3"])
 def test_c3_two_patch_step_vs_oracle(precision, tmp_path, monkeypatch):
     """C3 shape (256x256 crops of a 512 canvas, L=16, 4x256), 2 patches, non-zero warps on both.
-    bf16x3-w12: the opt-in 12-wave k_step3 (MARF_S3_NW=12: 192-pixel tiles, so each 65,536-pixel
-    crop ends in a padded tile of 64 slots).
+    bf16x3-step3: the opt-in two-waves-per-SIMD kernel (MARF_STEP3=1).
     rgb <= 1e-5 abs and loss vs oracle.PlanarStep (fp32 <= 1e-6 rel).  Gradients against the
     float64 reference ops: fp32 within 1e-5 relative to their max OR within 2x the reference's own
     fp32 error, whichever is larger (_compare_step); bf16x3 (the bench recipe) within 1e-2 (north_star
     bf16 bound) AND within 2x the reference's own fp32 error (measured: MLP 4.9e-4 vs the
     reference's 4.7e-4; d warp 6.9e-3 vs 5.3e-3 -- a 2 x 65,536-pixel sum that cancels)."""
-    if precision == "bf16x3-w12":
-        monkeypatch.setenv("MARF_S3_NW", "12")
+    if precision == "bf16x3-step3":
+        monkeypatch.setenv("MARF_STEP3", "1")
         precision = "bf16x3"
     m, var, inputs = _synthetic_setup(precision, tmp_path, 2, 256, 16, [256] * 4)
     o = _compare_step(m, var, inputs, precision, 5)
