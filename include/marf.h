@@ -117,6 +117,9 @@ size_t marf_net_packed_bytes(const marf_net* net);
 /* Name of the kernel that runs this net's fused training step ("k_step2", "k_step3", "k_mlp_step"),
  * fixed at net creation (no reference counterpart: measurement and test bookkeeping). */
 const char* marf_net_step_kernel(const marf_net* net);
+/* Layer l's parameters in the flat vector: W_l [dims[l+1]][dims[l]] then b_l, from *off, *len floats. */
+int marf_net_layer_count(const marf_net* net);
+int marf_net_layer_span(const marf_net* net, int l, long long* off, long long* len);
 /* Pipelined weight gradients of the fused step (no reference counterpart: scheduling only; the
  * reference's loss.all.backward() at model/planar.py:196 computes the same sums).  mode 0 = off
  * (default; env MARF_PIPE at net creation), 1 = on at any size, -1 = on for large steps.  When on,
@@ -168,6 +171,28 @@ int marf_step_forward(const marf_net* net, const marf_geometry* geo, const marf_
 int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void* d_saved, const float* d_h_params,
                        int lie_batch, const float* d_gout, const float* d_loss_out, float* d_dparams, float* d_dh,
                        void* stream);
+/* As marf_step_backward; layer_events[l] (hipEvent_t, n_layers entries, NULL entries skipped) is
+ * recorded on the stream as soon as layer l's gradient in d_dparams is final.  The layers finish
+ * last layer first, layer 0 last (the order a bucketed all-reduce consumes them). */
+int marf_step_backward_ev(const marf_net* net, const marf_geometry* geo, const void* d_saved, const float* d_h_params,
+                          int lie_batch, const float* d_gout, const float* d_loss_out, float* d_dparams, float* d_dh,
+                          void* const* layer_events, void* stream);
+
+/* ---- MLP-gradient exchange of the patch-sharded step (the reference is
+ * single-GPU, options.py:117-120, so this replaces no reference call: it is the one collective the
+ * sharding adds).  RCCL over xGMI, librccl.so opened at first use.  marf_comm_unique_id fills 128
+ * bytes on one rank (the host shares them with the others); marf_comm_create joins rank `rank` of
+ * `nranks` on `device`.  marf_allreduce_grads sums a flat fp32 gradient in place on `stream`;
+ * marf_allreduce_grads_layers sums each layer's span (marf_net_layer_span) on the communicator's
+ * own stream after its marf_step_backward_ev event, so the exchange overlaps the remaining weight
+ * gradients, and makes `stream` wait for the last one. */
+typedef struct marf_comm marf_comm;
+int marf_comm_unique_id(void* out, size_t cap);
+int marf_comm_create(const void* unique_id, int nranks, int rank, int device, marf_comm** out);
+void marf_comm_destroy(marf_comm* comm);
+int marf_allreduce_grads(marf_comm* comm, float* d_flat, size_t n, void* stream);
+int marf_allreduce_grads_layers(marf_comm* comm, const marf_net* net, float* d_dparams, void* const* layer_events,
+                                void* stream);
 
 /* ---- Masked MSE (Graph.mse_loss, model/planar.py:382-391).  pred [B][Np][3] (MLP layout),
  * gt [B][3][Np], mask [B][1][Np] or NULL (plain mean).  d_out[3]: loss, denominator used,

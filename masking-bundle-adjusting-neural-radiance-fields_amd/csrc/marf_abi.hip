@@ -98,26 +98,28 @@ static bool step2_env_enabled() {
 
 int marf_step3_wave_lds_bytes();
 
-// variant 3 (marf_step3.hip): 16 pixels per wave on 16x16x32 MFMAs, 8 waves, 32 KB stages of
-// 16-row tiles -- layer 0: r0 row tiles of nk0 k-steps (nb = ceil(L / 8) band steps + the raw
-// coordinates); hidden / adjoint: two row tiles of 8 k-steps; the last-layer dgrad: every row tile
+// variant 3 (marf_step3.hip): k_step2's arithmetic on 16 pixels per wave (16x16x32 MFMAs, 8 waves,
+// 128-pixel block tiles as k_step2), 32 KB stages of 16-row tiles -- layer 0: r0 row tiles of nk0
+// operand pairs (k_step2's ng = ceil(L / 4) band chunks + the raw chunk, two per pair); hidden /
+// adjoint: two row tiles of 8 pairs; the last-layer dgrad: every row tile.  The adjoint has ng band
+// tiles + the raw tile.  Loss, dH and dW_last partials are k_step2's: one per 32-pixel set (PX).
 static void plan_step3_net(marf_net* n) {
     Step2NetPlan& q = n->s2;
     const int nl = n->n_layers;
     q.variant = 3;
     q.HM = 256;
     q.NS = 1;
-    q.PX = 16;
+    q.PX = 32;
     q.NW = 8;
-    q.TPX = q.NW * q.PX;
+    q.TPX = 128;
     q.nslot = 3;
     q.MAXR = 4;
     q.NMW = 4;
     q.slot = 32768;
-    const int nb = (n->L + 7) / 8;
-    q.nk0 = nb + 1;
-    q.nta = 2 * nb + 1;
-    q.nk0w = (n->L + 3) / 4 + 1;
+    const int ng = (n->L + 3) / 4;
+    q.nk0 = (ng + 2) / 2;
+    q.nta = ng + 1;
+    q.nk0w = ng + 1;
     q.ldf0 = (int)rup(16 * q.nk0w, 32);
     q.Kl = n->Kp[nl - 1];
     int bo = 0;
@@ -208,6 +210,8 @@ static void plan_step2_net(marf_net* n) {
 extern "C" {
 
 const char* marf_last_error(void) { return g_err.c_str(); }
+// (for the other translation units: marf_comm.hip)
+int marf_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 
 // Diagnostic builds only: device buffer [n_tiles][32] for the fused step's phase stamps.
 void marf_debug_set_stamps(void* d_stamps) { g_stamps = (unsigned long long*)d_stamps; }
@@ -508,6 +512,13 @@ int marf_net_set_pipeline(marf_net* net, int mode, int wg_blocks, int piece_tile
 }
 long long marf_net_param_count(const marf_net* net) { return net ? net->param_count : -1; }
 size_t marf_net_packed_bytes(const marf_net* net) { return net ? net->packed_bytes : 0; }
+int marf_net_layer_count(const marf_net* net) { return net ? net->n_layers : 0; }
+int marf_net_layer_span(const marf_net* net, int l, long long* off, long long* len) {
+    if (!net || l < 0 || l >= net->n_layers || !off || !len) return fail(MARF_ERR_INVALID, "net_layer_span: bad arguments");
+    *off = net->w_off[l];
+    *len = (long long)net->dims[l + 1] * net->dims[l] + net->dims[l + 1];  // W_l then b_l
+    return MARF_OK;
+}
 const char* marf_net_step_kernel(const marf_net* net) {
     if (!net) return "";
     if (net->s2.variant == 3) return "k_step3";
@@ -843,7 +854,7 @@ struct PipePlan {
 
 struct Step2BufPlan {
     size_t feat[MARF_MAX_LAYERS], dz[MARF_MAX_LAYERS];
-    size_t dH, loss, blast, wlast, dummy, c2f, kmap, part, bpart, total;
+    size_t dH, loss, blast, wlast, dummy, xbuf, c2f, kmap, part, bpart, total;
     size_t partl[MARF_MAX_LAYERS], bpartl[MARF_MAX_LAYERS];  // pipelined: per-layer split-K partials
     int grid, n_tiles;
     int nblk;  // per-block partial sets of the step kernel (all pieces' blocks)
@@ -995,6 +1006,9 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
     off += rup((long long)p.nblk * 3 * q.Kl * 4, 256);
     p.dummy = off;
     off += rup((long long)p.grid * q.NW * 4096, 256);  // 64 B per lane
+    // k_step3: the dW_last partials a first-half wave hands to its second-half partner (12 x 16 B per lane)
+    p.xbuf = off;
+    if (q.variant == 3) off += rup((long long)p.grid * 4 * 12 * 32 * 16, 256);
     p.c2f = off;
     off += 256;
     p.kmap = off;  // the layer-0 column map, copied from the packed buffer by the forward
@@ -1119,6 +1133,7 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     a.Kl = q.Kl;
     a.c2f_w = (const float*)(sv + p.c2f);
     a.dummy = (float*)(sv + p.dummy);
+    a.xbuf = (float*)(sv + p.xbuf);
     a.stamps = g_stamps;
     a.n_tiles = p.n_tiles;
     // LDS layout
@@ -1184,9 +1199,15 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     return MARF_OK;
 }
 
+// record layer l's "gradient final" event, if the caller passed one
+static int mark_layer(const void* const* ev, int l, hipStream_t s) {
+    if (ev && ev[l]) HIPCHK(hipEventRecord((hipEvent_t)ev[l], s), "step_backward: layer event");
+    return MARF_OK;
+}
+
 static int step2_backward(const marf_net* net, const marf_geometry* geo, const void* d_saved,
                           const float* d_h_params, int lie_batch, const float* d_gout, const float* d_loss_out,
-                          float* d_dparams, float* d_dh, hipStream_t s) {
+                          float* d_dparams, float* d_dh, hipStream_t s, const void* const* ev) {
     const Step2NetPlan& q = net->s2;
     GeoDev g;
     int rc = make_geo(geo, g, q.TPX);
@@ -1198,9 +1219,21 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
     float* bpart = (float*)(sv + p.bpart);
     const float* denom = d_loss_out + 1;
     const int nl = net->n_layers;
+    // the layers finish in reverse order (last layer first, layer 0 last), each marked by its event,
+    // so that a bucketed all-reduce of finished layers overlaps the remaining weight gradients
+    if (d_dparams) {
+        const int l = nl - 1;
+        MarfProfScope ps("wgrad_last_reduce", s);
+        HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.wlast), (const float*)(sv + p.blast), p.nblk, 3, q.Kl, 3,
+                                        net->dims[l], d_dparams + net->w_off[l], d_dparams + net->b_off[l], s, d_gout,
+                                        denom, part),
+               "step_backward last reduce");
+        rc = mark_layer(ev, l, s);
+        if (rc) return rc;
+    }
     if (d_dparams && p.pipe.on) {  // the split-K partials were computed beside the step kernel
         const int* kmap = (const int*)(sv + p.kmap);
-        for (int l = 0; l < nl - 1; ++l) {
+        for (int l = nl - 2; l >= 0; --l) {
             const int K = l == 0 ? q.ldf0 : net->Kp[l];
             MarfProfScope ps("wgrad_reduce", s);
             HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.partl[l]), (const float*)(sv + p.bpartl[l]),
@@ -1208,13 +1241,15 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                                             d_dparams + net->w_off[l], d_dparams + net->b_off[l], s, d_gout, denom,
                                             nullptr, l == 0 ? kmap : nullptr),
                    "step_backward wgrad reduce (pipelined)");
+            rc = mark_layer(ev, l, s);
+            if (rc) return rc;
         }
     } else if (d_dparams) {
         const long long chunk = wgrad_chunk(p.S);
         const int n_chunks = (int)((p.S + chunk - 1) / chunk);
         const int* kmap = (const int*)(sv + p.kmap);
         const bool f0 = l0_recompute(net, g, p.S);
-        for (int l = 0; l < nl - 1; ++l) {
+        for (int l = nl - 2; l >= 0; --l) {
             const int K = l == 0 ? q.ldf0 : net->Kp[l];
             {
                 MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
@@ -1234,15 +1269,9 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                                                 nullptr, l == 0 ? kmap : nullptr),
                        "step_backward wgrad reduce");
             }
+            rc = mark_layer(ev, l, s);
+            if (rc) return rc;
         }
-    }
-    if (d_dparams) {
-        const int l = nl - 1;
-        MarfProfScope ps("wgrad_last_reduce", s);
-        HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.wlast), (const float*)(sv + p.blast), p.nblk, 3, q.Kl, 3,
-                                        net->dims[l], d_dparams + net->w_off[l], d_dparams + net->b_off[l], s, d_gout,
-                                        denom, part),
-               "step_backward last reduce");
     }
     if (d_dh) {
         MarfProfScope ps("warp_bwd", s);
@@ -1340,11 +1369,20 @@ int marf_step_forward(const marf_net* net, const marf_geometry* geo, const marf_
 int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void* d_saved, const float* d_h_params,
                        int lie_batch, const float* d_gout, const float* d_loss_out, float* d_dparams, float* d_dh,
                        void* stream) {
+    return marf_step_backward_ev(net, geo, d_saved, d_h_params, lie_batch, d_gout, d_loss_out, d_dparams, d_dh, nullptr,
+                                 stream);
+}
+
+int marf_step_backward_ev(const marf_net* net, const marf_geometry* geo, const void* d_saved, const float* d_h_params,
+                          int lie_batch, const float* d_gout, const float* d_loss_out, float* d_dparams, float* d_dh,
+                          void* const* layer_events, void* stream) {
+    const void* const* ev = (const void* const*)layer_events;
     if (!net || !d_saved || !d_gout || !d_loss_out) return fail(MARF_ERR_INVALID, "step_backward: NULL argument");
     if (!geo || geo->mode == MARF_GEO_COORDS) return fail(MARF_ERR_INVALID, "step_backward: needs a pixel-grid geometry");
     if (d_dh && !d_h_params) return fail(MARF_ERR_INVALID, "step_backward: d_dh requested without the warp parameters");
     hipStream_t s = (hipStream_t)stream;
-    if (use_step2(net)) return step2_backward(net, geo, d_saved, d_h_params, lie_batch, d_gout, d_loss_out, d_dparams, d_dh, s);
+    if (use_step2(net))
+        return step2_backward(net, geo, d_saved, d_h_params, lie_batch, d_gout, d_loss_out, d_dparams, d_dh, s, ev);
     GeoDev g;
     int rc = make_geo(geo, g, MARF_TILE_PAD);
     if (rc) return rc;
@@ -1356,8 +1394,18 @@ int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void
     float* bpart = (float*)(sv + p.bpart);
     const float* denom = d_loss_out + 1;
     const int nl = net->n_layers;
-    if (d_dparams) {
-        for (int l = 0; l < nl - 1; ++l) {
+    if (d_dparams) {  // last layer first, then l = nl-2 .. 0, each marked by its event (as step2_backward)
+        {
+            const int l = nl - 1;
+            MarfProfScope ps("wgrad_last_reduce", s);
+            HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.wlast), (const float*)(sv + p.blast), p.n_tiles, 3,
+                                            net->Kp[l], 3, net->dims[l], d_dparams + net->w_off[l],
+                                            d_dparams + net->b_off[l], s, d_gout, denom, part),
+                   "step_backward last reduce");
+            rc = mark_layer(ev, l, s);
+            if (rc) return rc;
+        }
+        for (int l = nl - 2; l >= 0; --l) {
             {
                 MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
                 HIPCHK(marf_launch_wgrad(net->kdt, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], net->Kp[l], S,
@@ -1371,13 +1419,9 @@ int marf_step_backward(const marf_net* net, const marf_geometry* geo, const void
                                                 d_gout, denom),
                        "step_backward wgrad reduce");
             }
+            rc = mark_layer(ev, l, s);
+            if (rc) return rc;
         }
-        const int l = nl - 1;
-        MarfProfScope ps("wgrad_last_reduce", s);
-        HIPCHK(marf_launch_wgrad_reduce((const float*)(sv + p.wlast), (const float*)(sv + p.blast), p.n_tiles, 3,
-                                        net->Kp[l], 3, net->dims[l], d_dparams + net->w_off[l],
-                                        d_dparams + net->b_off[l], s, d_gout, denom, part),
-               "step_backward last reduce");
     }
     if (d_dh) {
         MarfProfScope ps("warp_bwd", s);

@@ -105,6 +105,7 @@ struct Step2Args {
     int Kl;                          // padded input width of the last layer
     const float* c2f_w;              // [L] band weights of this step
     float* dummy;                    // [grid][NW][ST][64][2] store sink
+    float* xbuf;                     // k_step3: [grid][4][12][32][4] dW_last partials handed between waves
     unsigned long long* stamps;      // diagnostic builds (MARF_STAMPS): [grid][8] cycle totals of wave 0
     int tile0, n_tiles;              // this launch's block tiles [tile0, n_tiles) of 32 * NW pixel slots
     int fwd_only;                    // render: forward stages only, rgb out, nothing saved

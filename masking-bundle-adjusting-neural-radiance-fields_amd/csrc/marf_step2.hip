@@ -48,24 +48,15 @@ MARF_DEV void s2_glds4(const void* src, unsigned lds) {
 typedef uint32_t s2_u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t s2_u32x4 __attribute__((ext_vector_type(4)));
 MARF_DEV void s2_st8(void* dst, uint32_t a, uint32_t b) {
-#ifdef S2_DIAG_NOSTORE
-    return;
-#endif
     const s2_u32x2 v = {a, b};
     asm volatile("global_store_dwordx2 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
 MARF_DEV void s2_st16(void* dst, uint4 u) {
-#ifdef S2_DIAG_NOSTORE
-    return;
-#endif
     const s2_u32x4 v = {u.x, u.y, u.z, u.w};
     asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
 template <int OFF>
 MARF_DEV void s2_st16o(void* base, uint4 u) {  // 16 B at base + OFF bytes (instruction offset)
-#ifdef S2_DIAG_NOSTORE
-    return;
-#endif
     const s2_u32x4 v = {u.x, u.y, u.z, u.w};
     asm volatile("global_store_dwordx4 %0, %1, off offset:%2\n\ts_nop 1" ::"v"(base), "v"(v), "n"(OFF) : "memory");
 }
@@ -274,16 +265,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         static_assert(j < C::PER_DMA && C::PER_DMA <= 8, "piece index");
         const char* va = j < 4 ? dma_va0 : dma_va1;
         const unsigned m = dma_m0 + (j < 4 ? 0u : 4096u);
-#ifndef S2_DIAG_NODMA
         unsigned keep;  // m0 is reserved to the compiler: saved and restored around the piece
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off offset:%3\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep)
                      : "v"(va), "s"(m), "n"((j & 3) * 1024)
                      : "memory");
-#else
-        (void)va;
-        (void)m;
-#endif
     };
     auto dma_burst = [&]() { s2_sfor<C::PER_DMA>([&](auto jc) { dma_piece(jc); }); };
     // vm-op accounting for the ring waits: st_cur counts the store instructions a wave issued since
@@ -314,9 +300,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         st_prev = st_cur;
         st_cur = 0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#ifndef S2_DIAG_NOBAR  // (S2_DIAG_* : timing-only diagnostic builds, results invalid)
         __builtin_amdgcn_s_barrier();
-#endif
         asm volatile("" ::: "memory");
         S2T_END(0);
         S2T_BEGIN(1);
@@ -420,11 +404,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         s2_sfor<NK>([&](auto ksc) {
             constexpr int ks = decltype(ksc)::value;
             constexpr int u = ks & 3;
-#ifdef S2_DIAG_NOALDS  // timing only: the A fragments are not refilled from LDS (results invalid)
-            constexpr bool refill = false;
-#else
             constexpr bool refill = ks + P < NK;
-#endif
             const bool live = NK != C::NK0 || ks < nk;
             auto piece = [&]() { piece_at(ksc, nk_tag, pieces_tag); };
             __builtin_amdgcn_sched_barrier(0);
@@ -444,9 +424,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 if constexpr (refill) A0[u] = ah[(ks + P) * 64];
                 __builtin_amdgcn_sched_barrier(0);
                 if (live) {
-#ifndef S2_BWD_NO_W_LO  // numerics experiment: dgrad with W_hi^T only
                     mf(acc, A1[u], Bhi[ks].f);
-#endif
                     hook(ksc, P1());
                 }
                 if constexpr (refill) A1[u] = al[(ks + P) * 64];
@@ -458,16 +436,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (live) {
-#ifndef S2_FWD_NO_ACT_LO  // numerics experiment: activations carried as bf16 hi only
                     mf(acc, A0[u], Blo[ks].f);
-#endif
                     hook(ksc, P1());
                 }
                 if constexpr (refill) A0[u] = ah[(ks + P) * 64];
                 __builtin_amdgcn_sched_barrier(0);
-#ifndef S2_FWD_NO_W_LO  // numerics experiment: forward weights bf16 hi only
                 if (live) mf(acc, A1[u], Bhi[ks].f);
-#endif
                 if constexpr (refill) A1[u] = al[(ks + P) * 64];
                 if (live) piece();
             }
@@ -511,9 +485,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     // bf16 pair of registers e-1, e (fpack)
     auto frelu = [&](const f32x16& pa, auto ec) {
         constexpr int e = decltype(ec)::value;
-#ifdef S2_DIAG_NOEPI
-        return;
-#endif
         // relu as a signed-integer max with 0 (negative floats and -0 are negative integers: exactly
         // x > 0 ? x : 0); the mask bits come from the packed bf16 pair (mask_pair)
         float x;
@@ -540,9 +511,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     //  even, as s2_pk)
     auto fpack = [&](auto ec) {
         constexpr int e = decltype(ec)::value;
-#ifdef S2_DIAG_NOEPI
-        return;
-#endif
         if constexpr (e & 1) {
             if constexpr (SPLIT) {
                 uint32_t w, wl, t0, t1;
@@ -572,9 +540,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     auto fpackA = [&](auto ec) {
         constexpr int e = decltype(ec)::value;
         static_assert(e & 1, "odd step");
-#ifdef S2_DIAG_NOEPI
-        return;
-#endif
         uint32_t w;
         float t0, t1;
         asm volatile(
@@ -591,9 +556,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     auto fpackB = [&](auto ec) {
         constexpr int e = decltype(ec)::value;
         static_assert(e & 1, "odd step");
-#ifdef S2_DIAG_NOEPI
-        return;
-#endif
         uint32_t wl;
         float r0, r1;
         asm volatile(
@@ -609,27 +571,27 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         fpack(ec);
     };
     // forward finish of tile rt: operand fragments of k-steps 2 rt, 2 rt + 1, mask word, 2 stores
-    auto ffinish = [&](int l, auto rtc, bool save, u16* srow, uint32_t* mks) {
+    // (last: the layer's last row tile -- an odd row-tile count (a width of 32 mod 64) stores its
+    //  mask word without the odd partner's bits)
+    auto ffinish = [&](int l, auto rtc, bool save, u16* srow, uint32_t* mks, bool last) {
         constexpr int rt = decltype(rtc)::value;
-#ifdef S2_DIAG_NOEPI
-        return;
-#endif
         Oh[2 * rt].u = make_uint4(ep.hw[0], ep.hw[1], ep.hw[2], ep.hw[3]);
         Oh[2 * rt + 1].u = make_uint4(ep.hw[4], ep.hw[5], ep.hw[6], ep.hw[7]);
         if constexpr (SPLIT) {
             Ol[2 * rt].u = make_uint4(ep.lw[0], ep.lw[1], ep.lw[2], ep.lw[3]);
             Ol[2 * rt + 1].u = make_uint4(ep.lw[4], ep.lw[5], ep.lw[6], ep.lw[7]);
         }
-        if constexpr ((rt & 1) == 0) mpend = ep.bits << 8;
-        else mks[(l * C::NMW + (rt >> 1)) * 64 + lane] = mpend | ep.bits;
+        if constexpr ((rt & 1) == 0) {
+            mpend = ep.bits << 8;
+            if (last) mks[(l * C::NMW + (rt >> 1)) * 64 + lane] = mpend;
+        } else {
+            mks[(l * C::NMW + (rt >> 1)) * 64 + lane] = mpend | ep.bits;
+        }
         if (save) store_rt(srow, rtc, Oh[2 * rt], Oh[2 * rt + 1]);
     };
     // dgrad step e: dz = acc * relu'(z) with the mask word e.mw
     auto bstep = [&](EpSt& es, const f32x16& pa, auto ec, auto rtc) {
         constexpr int e = decltype(ec)::value;
-#ifdef S2_DIAG_NOEPI
-        return;
-#endif
         constexpr int rt = decltype(rtc)::value;
         // (mask_pair's layout: pair e >> 1, odd elements in the upper stream, even row tiles << 8)
         constexpr int bit = 16 * (e & 1) + 8 * (1 - (rt & 1)) + 7 - (e >> 1);
@@ -649,9 +611,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     };
     auto bfinish = [&](EpSt& es, S2Frag* O, auto rtc, u16* row0) {
         constexpr int rt = decltype(rtc)::value;
-#ifdef S2_DIAG_NOEPI
-        return;
-#endif
         O[2 * rt].u = make_uint4(es.hw[0], es.hw[1], es.hw[2], es.hw[3]);
         O[2 * rt + 1].u = make_uint4(es.hw[4], es.hw[5], es.hw[6], es.hw[7]);
         store_rt(row0, rtc, O[2 * rt], O[2 * rt + 1]);
@@ -764,11 +723,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 constexpr bool SPLITPK = SPLIT && MS == 1 && decltype(nk_tag)::value == NKH;  // hidden, split recipe
                 const int nrt = ly_int(l, 0);
                 const bool save = l + 1 < nl - 1 && !a.fwd_only;
-#ifdef S2_DIAG_CONTIG  // timing only: each store 1 KB contiguous (wrong layout; results invalid)
-                u16* srow = save ? ly_ptr(l + 1, 0) + (myslot - pxl) * ly_int(l + 1, 3) + 8 * lane : nullptr;
-#else
                 u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) + 8 * h : nullptr;
-#endif
                 const int boff = ly_int(l, 2);
                 const char* slot0 = nullptr;
                 s2_sfor<NRT>([&](auto rtc) {
@@ -823,14 +778,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                             });
                             S2T_END(13);
                             S2T_BEGIN(10);
-                            ffinish(l, std::integral_constant<int, rt - 1>(), save, srow, mks);
+                            ffinish(l, std::integral_constant<int, rt - 1>(), save, srow, mks, false);
                             S2T_END(10);
                         }
                         if (rt == nrt - 1) {
                             S2T_BEGIN(13);
                             ep.bits = 0;
                             s2_sfor<16>([&](auto ec) { fstep(cur, ec); });
-                            ffinish(l, rtc, save, srow, mks);
+                            ffinish(l, rtc, save, srow, mks, true);
                             S2T_END(13);
                         }
                     } else {
@@ -990,11 +945,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const int nrt = ly_int(nl - 1, 1);
             u16* brow[NS];
             s2_sfor<NS>([&](auto sc) {
-#ifdef S2_DIAG_CONTIG
-                brow[decltype(sc)::value] = ly_ptr(nl - 1, 1) + (myslot_of(decltype(sc)::value) - pxl) * ly_int(nl - 1, 4) + 8 * lane;
-#else
                 brow[decltype(sc)::value] = ly_ptr(nl - 1, 1) + myslot_of(decltype(sc)::value) * ly_int(nl - 1, 4) + 8 * h;
-#endif
             });
             S2Frag gB[NS];
             s2_sfor<NS>([&](auto sc) { gB[decltype(sc)::value] = ss[decltype(sc)::value].g; });
@@ -1045,11 +996,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const int nrt = ly_int(l, 1);
             u16* brow[NS];
             s2_sfor<NS>([&](auto sc) {
-#ifdef S2_DIAG_CONTIG
-                brow[decltype(sc)::value] = ly_ptr(l, 1) + (myslot_of(decltype(sc)::value) - pxl) * ly_int(l, 4) + 8 * lane;
-#else
                 brow[decltype(sc)::value] = ly_ptr(l, 1) + myslot_of(decltype(sc)::value) * ly_int(l, 4) + 8 * h;
-#endif
             });
             s2_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;

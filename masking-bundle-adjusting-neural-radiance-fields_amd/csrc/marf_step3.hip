@@ -1,30 +1,43 @@
-// marf_step3.hip -- the fused training step of the split-bf16 recipe at TWO waves per SIMD (gfx950).
+// marf_step3.hip -- the fused training step of the split-bf16 recipe at TWO waves per SIMD (gfx950),
+// bit-identical to k_step2 (marf_step2.hip, variant 1).
 //
-// Same contract and saved tensors as k_step2 (marf_step2.hip, variant 1): per pixel grid -> sl(3)
-// warp -> posenc + c2f -> MLP forward (hi*hi + hi*lo + lo*hi, fp32 accumulation) -> sigmoid ->
-// masked-MSE partial -> d rgb -> dgrad chain (W_hi^T dz + W_lo^T dz) -> posenc / warp adjoint
-// (model/planar.py:329-391, warp.py:33-81), writing feat_l / dz_l for the weight-gradient kernels.
-// What changes is the shape on the CU:
+// Same contract and saved tensors as k_step2: per pixel grid -> sl(3) warp -> posenc + c2f -> MLP
+// forward (hi*hi + hi*lo + lo*hi, fp32 accumulation) -> sigmoid -> masked-MSE partial -> d rgb ->
+// dgrad chain (W_hi^T dz + W_lo^T dz) -> posenc / warp adjoint (model/planar.py:329-391,
+// warp.py:33-81), writing feat_l / dz_l for the weight-gradient kernels.  Every fp32 operation on
+// the way happens in k_step2's order, so rgb, loss and every gradient carry k_step2's bits (and
+// with them its seed-3 run).  What changes is the shape on the CU:
 //
-//   * one wave owns 16 pixels (not 32) and computes every feature of them with
-//     v_mfma_f32_16x16x32_bf16: a 16-row accumulator tile holds, per lane (pixel l & 15, group
-//     l >> 4), rows 4 (l >> 4) + 0..3; the pair of row tiles (2s, 2s + 1), packed to bf16 hi + lo,
-//     is k-step s of the next layer's B operand as it stands (k order permuted inside the step:
-//     position 8 g + j <-> feature 32 s + 4 g + j for j < 4, 32 s + 16 + 4 g + j - 4 otherwise;
-//     the weights are packed in the same order, k_pack3).  Half the pixels halve the activation
-//     registers (hi + lo of a 256-wide layer: 64 instead of 128), so a wave fits in 256 registers
-//     and the 512-thread block (8 waves, one per CU) runs TWO waves per SIMD: while one wave waits
-//     (ring, barrier, an epilogue's dependency) the other issues MFMAs.
-//   * the weights stream through the same 3-slot LDS ring (one 32 KB slot = 32 rows of one layer,
-//     hi then lo, filled by global_load_lds_dwordx4 two stages ahead, 4 pieces per wave).
-//   * ReLU masks: 4 bits per lane and row tile, 2 words per lane and layer, in wave-private LDS.
-//   * one pixel set per dgrad pass (the two-set dgrad of k_step2 is not needed at two waves per
-//     SIMD: the LDS A-fragment reads of a dgrad stage are 2 KB per 2 MFMAs and wave).
+//   * one wave owns 16 pixels (not 32) on v_mfma_f32_16x16x32_bf16, so a wave's operands fit in
+//     256 registers and the 512-thread block (8 waves, one per CU) runs TWO waves per SIMD.
+//   * k_step2 accumulates each output over 16-k chunks c with one 32x32x16 MFMA per term: forward
+//     hh(c), hl(c), lh(c) (hi.hi, hi.lo, lo.hi), dgrad hd(c), ld(c) (W_hi^T dz, W_lo^T dz).  A
+//     16x16x32 MFMA adds its two 16-k halves (lane groups 0-1, then 2-3) in order, each exactly as
+//     a 32x32x16 MFMA would (tools/mfma_compose_probe.hip: 0 of 12,288 outputs differ), so two
+//     consecutive terms make one MFMA: per pair of chunks (2s, 2s+1)
+//       forward  [hh(2s) | hl(2s)], [lh(2s) | hh(2s+1)], [hl(2s+1) | lh(2s+1)]   (3 MFMAs, as k_step2)
+//       dgrad    [hd(2s) | ld(2s)], [hd(2s+1) | ld(2s+1)]                          (2 MFMAs, as k_step2)
+//     The lane group g of an operand pair holds chunk 2s + (g >> 1) at k_step2's position
+//     8 (g & 1) + j, i.e. feature F(s, g, j) = 32 s + 16 (g >> 1) + 8 (j >> 2) + 4 (g & 1) + (j & 3)
+//     (k_step2's s2_kperm).  The output row tiles are permuted to match (s3_mrow), so a pair of
+//     16-row accumulator tiles packed to bf16 is operand pair s as it stands (H: hi words, L: lo).
+//     The B operands of the composite MFMAs are H / L with halves exchanged: one v_permlane32_swap
+//     per dword builds B1 = [H.h0 | L.h0] and B3 = [L.h1 | H.h1] (forward; the middle MFMA takes
+//     H = [B1.h0 | B3.h1], a select), or D1 = [D.h0 | D.h0] and D2 = [D.h1 | D.h1] (dgrad).  The A
+//     operands are the packed hi / lo fragments read with per-lane addresses (3 reads per forward
+//     pair, 2 per dgrad pair).
+//   * reductions over pixels are k_step2's 32-pixel ones: the waves w and w + 4 (one SIMD) own the
+//     two halves of k_step2's wave W = w: the last-layer weight gradient runs as one K = 32-pixel
+//     chain, the first half from 0 (stage L), the second half from that partial (stage L + 1,
+//     handed over through a per-block global buffer, xbuf); the dH partial and the loss / bias
+//     sums gather the pair's 32 pixels in LDS and reduce them with k_step2's DPP tree.
+//   * the weights stream through a 3-slot LDS ring (one 32 KB slot = 32 rows of one layer, hi then
+//     lo, filled by global_load_lds_dwordx4 two stages ahead, 4 pieces per wave).
 //
 // Memory ordering as in k_step2: all global traffic inside the tile loop is inline asm (LDS-DMA,
-// stores); each wave counts the store instructions it issues per stage and waits for a ring slot
-// with the vmcnt that leaves exactly the younger operations in flight.  Every counted store is
-// issued by every wave (lanes with nothing to store write a private sink), so the counts hold.
+// stores) except the xbuf loads; each wave counts the store instructions it issues per stage and
+// waits for a ring slot with the vmcnt that leaves exactly the younger operations in flight.
+// Every counted store is issued by every wave (lanes with nothing to store write a private sink).
 #include <type_traits>
 
 #include "marf_args.h"
@@ -33,18 +46,26 @@ namespace marf {
 namespace s3 {
 
 constexpr int PX = 16;                        // pixels per wave
+constexpr int NW = 8;                         // waves per block (two per SIMD)
+constexpr int TPX = NW * PX;                  // pixel slots per block tile (k_step2's)
 constexpr int HM = 256;                       // widest hidden layer
-constexpr int NKH = HM / 32;                  // k-steps (32 k) of a hidden-width operand
+constexpr int NPH = HM / 32;                  // operand pairs (two 16-k chunks) of a hidden-width input
 constexpr int NRT = HM / 16;                  // 16-row tiles of a hidden-width output
 constexpr int SLOT = 32768;                   // one ring slot = one program stage
 constexpr int LO = 16384;                     // byte offset of the lo fragments in a slot
-constexpr int PER_DMA = 4;                    // 1 KB DMA pieces per DMA wave and stage
-constexpr int NK0MAX = 5;                     // max layer-0 k-steps (L <= 32: 4 band steps + raw)
+constexpr int PER_DMA = 4;                    // 1 KB DMA pieces per wave and stage
+constexpr int NSLOT = 3;
+constexpr int NP0MAX = 5;                     // max layer-0 pairs (L <= 32: 8 band chunks + raw)
 constexpr int NML = 4;                        // max ReLU layers (nl <= 5)
-// wave-private LDS: g^T image (256 B), transpose scratch (1 KB), mask words [NML][2][64], dW_last [3][256]
+constexpr int XQ = 12;                        // 16-B pieces of a lane's dW_last partial (16 MFMAs x 3 rows)
+// wave-private LDS: g^T image [8][16] (256 B), transpose scratch (1 KB), mask words [NML][2][64],
+// dW_last [3][256] (second-half waves; a first-half wave's copy is its pair's exchange buffer)
 constexpr int W_GIMG = 0, W_SCR = 256, W_MASK = 1280, W_WLA = W_MASK + NML * 2 * 64 * 4;
 constexpr int WAVE_LDS = W_WLA + 3 * HM * 4;
-static_assert(SLOT % (PER_DMA * 1024) == 0, "ring geometry");
+// the pair exchange buffer (bytes): dH terms [9][32] fp32, loss sums [32] fp64 x 2, bias grads [3][32]
+constexpr int PB_DH = 0, PB_LSQ = 9 * 32 * 4, PB_LMS = PB_LSQ + 32 * 8, PB_BL = PB_LMS + 32 * 8;
+static_assert(PB_BL + 3 * 32 * 4 <= 3 * HM * 4, "pair buffer");
+static_assert(SLOT % (PER_DMA * 1024 * NW) == 0, "ring geometry");
 
 }  // namespace s3
 
@@ -64,17 +85,11 @@ MARF_DEV void s3_glds4(const void* src, unsigned lds) {
 }
 typedef uint32_t s3_u32x4 __attribute__((ext_vector_type(4)));
 MARF_DEV void s3_st16(void* dst, uint4 u) {
-#ifdef S3_AB_NOSTORE  // timing-only A/B builds: no saved-tensor stores
-    return;
-#endif
     const s3_u32x4 v = {u.x, u.y, u.z, u.w};
     asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
 template <int OFF>
 MARF_DEV void s3_st16o(void* base, uint4 u) {  // 16 B at base + OFF bytes (instruction offset)
-#ifdef S3_AB_NOSTORE  // timing-only A/B builds: no saved-tensor stores
-    return;
-#endif
     const s3_u32x4 v = {u.x, u.y, u.z, u.w};
     asm volatile("global_store_dwordx4 %0, %1, off offset:%2\n\ts_nop 1" ::"v"(base), "v"(v), "n"(OFF) : "memory");
 }
@@ -113,17 +128,17 @@ MARF_DEV float s3_lo16(uint32_t w) { return __uint_as_float(w << 16); }
 MARF_DEV float s3_hi16(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 // relu as a signed-integer max with 0: exactly x > 0 ? x : +0 (negative floats and -0 are negative integers)
 MARF_DEV float s3_relu(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
-// 8 floats -> bf16 hi fragment + lo remainder fragment
-MARF_DEV void s3_split8(const float* x, S3Frag& hi, S3Frag& lo) {
-    hi.u = make_uint4(s3_pk(x[0], x[1]), s3_pk(x[2], x[3]), s3_pk(x[4], x[5]), s3_pk(x[6], x[7]));
-    const uint32_t w[4] = {hi.u.x, hi.u.y, hi.u.z, hi.u.w};
+// 8 floats -> bf16 hi words + lo remainder words (k_step2's s2_split8)
+MARF_DEV void s3_split8(const float* x, uint4& hi, uint4& lo) {
+    hi = make_uint4(s3_pk(x[0], x[1]), s3_pk(x[2], x[3]), s3_pk(x[4], x[5]), s3_pk(x[6], x[7]));
+    const uint32_t w[4] = {hi.x, hi.y, hi.z, hi.w};
     float r[8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         r[2 * q] = x[2 * q] - s3_lo16(w[q]);
         r[2 * q + 1] = x[2 * q + 1] - s3_hi16(w[q]);
     }
-    lo.u = make_uint4(s3_pk(r[0], r[1]), s3_pk(r[2], r[3]), s3_pk(r[4], r[5]), s3_pk(r[6], r[7]));
+    lo = make_uint4(s3_pk(r[0], r[1]), s3_pk(r[2], r[3]), s3_pk(r[4], r[5]), s3_pk(r[6], r[7]));
 }
 // per 16-bit half of a packed bf16 pair: (half != 0) at bits 0 and 16
 MARF_DEV uint32_t s3_nz_pair(uint32_t w) {
@@ -132,10 +147,47 @@ MARF_DEV uint32_t s3_nz_pair(uint32_t w) {
     return t;
 }
 
+// forward operand pair from its hi / lo words: B1 = [H.h0 | L.h0], B3 = [L.h1 | H.h1] (lo32: lane < 32)
+MARF_DEV void s3_fwd_pair(const uint4& H, const uint4& L, bool lo32, S3Frag& B1, S3Frag& B3) {
+    const uint32_t h[4] = {H.x, H.y, H.z, H.w}, l[4] = {L.x, L.y, L.z, L.w};
+    uint32_t b1[4], b3[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const auto p = __builtin_amdgcn_permlane32_swap(lo32 ? h[q] : l[q], lo32 ? l[q] : h[q], false, false);
+        b1[q] = p[0];
+        b3[q] = p[1];
+    }
+    B1.u = make_uint4(b1[0], b1[1], b1[2], b1[3]);
+    B3.u = make_uint4(b3[0], b3[1], b3[2], b3[3]);
+}
+// the hi words H = [B1.h0 | B3.h1] of a forward operand pair (volatile asm: rebuilt at each use, in
+// the MFMA gap -- a select the compiler may hoist would keep all of a layer's H words live, 32 VGPRs)
+MARF_DEV uint32_t s3_sel32(uint32_t lo_lanes, uint32_t hi_lanes) {
+    uint32_t r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(hi_lanes), "v"(lo_lanes), "s"(0xffffffffull));
+    return r;
+}
+MARF_DEV uint4 s3_mid(const S3Frag& B1, const S3Frag& B3) {
+    return make_uint4(s3_sel32(B1.u.x, B3.u.x), s3_sel32(B1.u.y, B3.u.y), s3_sel32(B1.u.z, B3.u.z),
+                      s3_sel32(B1.u.w, B3.u.w));
+}
+// dgrad operand pair: D1 = [D.h0 | D.h0], D2 = [D.h1 | D.h1]
+MARF_DEV void s3_bwd_pair(const uint4& D, S3Frag& D1, S3Frag& D2) {
+    const uint32_t d[4] = {D.x, D.y, D.z, D.w};
+    uint32_t a[4], b[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const auto p = __builtin_amdgcn_permlane32_swap(d[q], d[q], false, false);
+        a[q] = p[0];
+        b[q] = p[1];
+    }
+    D1.u = make_uint4(a[0], a[1], a[2], a[3]);
+    D2.u = make_uint4(b[0], b[1], b[2], b[3]);
+}
+
 // forward epilogue of one 16-row accumulator tile: ReLU, bf16 hi + lo of the 4 values (x0 x1 | x2 x3),
-// and the mask nibble (bits 0: x0, 1: x2, 16: x1, 17: x3), taken from the packed hi words: a value
-// is passed by the ReLU exactly when its bf16 hi is non-zero, except for 0 < z < 2^-133 (a zero hi,
-// as in k_step2)
+// and the mask nibble (bits 0: x0, 1: x2, 16: x1, 17: x3) from the packed hi words (k_step2's mask_pair:
+// a value passes the ReLU exactly when its bf16 hi is non-zero, except for 0 < z < 2^-133)
 struct S3Ep {
     uint32_t h0, h1, l0, l1, nib;
 };
@@ -175,28 +227,26 @@ MARF_DEV uint2 s3_bwd_ep(const f32x4& acc, uint32_t mw) {
     } while (0)
 #endif
 
-// NK0T: layer-0 k-steps (nb + 1 = ceil(L / 8) + 1); FULL: every hidden layer 256 wide.  Both make
-// the row-tile and k-step counts compile-time (no guards, no merges of partly written operand
-// arrays, which cost registers); <NK0MAX, false> is the generic instantiation.
-// NWT: waves per block -- 8 (two per SIMD, 3-slot ring) or 12 (three per SIMD, 2-slot ring: a
-// stage lasts long enough for its successor's DMA; 8 of the 12 waves issue it)
-template <int NK0T, bool FULL, int NWT>
-__global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
+// NP0T: layer-0 operand pairs (ceil((ceil(L / 4) + 1) / 2)); FULL: every hidden layer 256 wide.
+// Both make the row-tile and pair counts compile-time; <NP0MAX, false> is the generic instantiation.
+template <int NP0T, bool FULL>
+__global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
     using namespace s3;
-    constexpr int NW = NWT;
-    constexpr int TPX = NW * PX;
-    constexpr int NSLOT = NW == 8 ? 3 : 2;
-    constexpr int NDW = SLOT / (PER_DMA * 1024);  // waves that issue the ring's DMA
-    static_assert(NW == 8 || NW == 12, "waves per block");
-    constexpr int NK0 = NK0T;
-    constexpr int NTA = 2 * (NK0 - 1) + 1;        // adjoint row tiles (max)
-    constexpr int R0F = (16 / NK0) & ~1;           // layer-0 row tiles per stage (FULL)
+    constexpr int NP0 = NP0T;
+    constexpr int NTA = 2 * NP0;                   // adjoint row tiles (max: ng band tiles + raw)
+    constexpr int R0F = (16 / NP0) & ~1;           // layer-0 row tiles per stage (FULL)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pxl = lane & 15, grp = lane >> 4;
+    const bool lo32 = lane < 32;
+    // k_step2's wave W = wave & 3 (its 32 pixels); this wave holds half (wave >> 2) of them, and its
+    // SIMD partner (wave ^ 4) the other half
+    const int W = wave & 3, half = wave >> 2, pblk = 2 * W + half;
     const int nl = a.nl, L = a.L;
-    const int nk0 = FULL ? NK0 : a.nk0, nb = nk0 - 1;
+    const int np0 = FULL ? NP0 : a.nk0;
+    const int ng = (L + 3) / 4;                    // k_step2's band chunks (then the raw chunk)
+    const bool odd_tail = ((ng + 1) & 1) != 0;     // the last layer-0 pair has no second chunk
 
     const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
     float* bias_l = reinterpret_cast<float*>(smem + a.lds_bias);
@@ -212,10 +262,11 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
         return reinterpret_cast<u16*>(lo | (hi << 32));
     };
     char* wpriv = smem + a.lds_wave + wave * a.lds_wave_bytes;
-    u16* gimg = reinterpret_cast<u16*>(wpriv + W_GIMG);        // [6][16] g hi / lo of the wave's pixels
+    u16* gimg = reinterpret_cast<u16*>(wpriv + W_GIMG);        // [8][16]: rows 0-2 g hi, 4-6 g lo
     u16* scr = reinterpret_cast<u16*>(wpriv + W_SCR);          // [16 px][32 features] transpose image
     uint32_t* mkl = reinterpret_cast<uint32_t*>(wpriv + W_MASK);  // [layer][word][lane]
-    float* wla = reinterpret_cast<float*>(wpriv + W_WLA);      // [3][Kl] dW_last of the wave
+    float* wla = reinterpret_cast<float*>(wpriv + W_WLA);      // [3][Kl] dW_last (second-half waves)
+    char* pbuf = smem + a.lds_wave + W * a.lds_wave_bytes + W_WLA;  // the pair's exchange buffer
     float* dmy = a.dummy + (((size_t)blockIdx.x * NW + wave) * 64 + lane) * 16;  // 64-B store sink per lane
 #ifdef MARF_STAMPS
     unsigned long long tacc[16] = {};
@@ -226,8 +277,9 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
     if ((int)threadIdx.x < 32) c2f_l[threadIdx.x] = (int)threadIdx.x < L ? a.c2f_w[threadIdx.x] : 0.f;
     for (int e = threadIdx.x; e < nl * (int)(sizeof(S2Layer) / 4); e += NW * 64)
         reinterpret_cast<uint32_t*>(lyr)[e] = reinterpret_cast<const uint32_t*>(a.layers)[e];
-    for (int e = lane; e < 3 * a.Kl; e += 64) wla[e] = 0.f;
-    for (int e = lane; e < 128; e += 64) reinterpret_cast<uint32_t*>(gimg)[e] = 0u;
+    if (half == 1)
+        for (int e = lane; e < 3 * a.Kl; e += 64) wla[e] = 0.f;
+    reinterpret_cast<uint32_t*>(gimg)[lane] = 0u;
 
     const int tpp = a.geo.Np_pad / TPX;  // block tiles per patch
     const int Np = a.geo.Np;
@@ -259,8 +311,7 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
     int dma_stage = 0, dma_ps = 0, dma_slot = 0;  // next DMA: block stage, program stage, slot
     unsigned dma_m0 = 0;
     const char* dma_va = nullptr;
-    const bool dma_wave = NDW == NW || wave < NDW;
-    const char* const prog_w = a.prog + (dma_wave ? wave : 0) * PER_DMA * 1024 + lane * 16;
+    const char* const prog_w = a.prog + wave * PER_DMA * 1024 + lane * 16;
     const unsigned lds_w = lds0 + wave * PER_DMA * 1024;
     auto dma_arm = [&]() {
         const int ps = dma_stage < total ? dma_ps : 0;  // past the end: refill from stage 0 (never read)
@@ -272,10 +323,6 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
     };
     auto dma_piece = [&](auto jc) {
         constexpr int j = decltype(jc)::value;
-#ifdef S3_AB_NODMA  // timing-only A/B builds (wrong results): no weight DMA
-        return;
-#endif
-        if (!dma_wave) return;
         const char* va = dma_va;
         const unsigned m = __builtin_amdgcn_readfirstlane(dma_m0);  // an SGPR even under pressure
         unsigned keep;  // m0 is reserved to the compiler: saved and restored around the piece
@@ -287,22 +334,14 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
     auto dma_burst = [&]() { s3_sfor<PER_DMA>([&](auto jc) { dma_piece(jc); }); };
     // The DMA of stage c was issued right after the barrier of stage c - 2; younger than it are the
     // stores of stage c - 2 (st_prev), the pieces of stage c + 1 and the stores of stage c - 1 (st_cur).
+    // xflush: this wave stored a dW_last partial its partner loads after the next barrier -- wait for
+    // every store before it.
     int st_cur = 0, st_prev = 0;
+    bool xflush = false;
     auto wait_ring = [&]() {
-#ifdef S3_AB_NOWAIT  // timing-only A/B builds (wrong results): no ring wait
-        return;
-#endif
-        if constexpr (NSLOT == 2) {  // (every wave: the next tile's inputs are counted in as well)
-            // 2-slot ring: the DMA of stage c went out in stage c - 1; younger: that stage's stores
-            const int y = st_cur;
-            if (y >= 16) s3_wait_vm<16>();
-            else if (y >= 12) s3_wait_vm<12>();
-            else if (y >= 8) s3_wait_vm<8>();
-            else if (y >= 6) s3_wait_vm<6>();
-            else if (y >= 4) s3_wait_vm<4>();
-            else if (y >= 2) s3_wait_vm<2>();
-            else if (y >= 1) s3_wait_vm<1>();
-            else s3_wait_vm<0>();
+        if (xflush) {
+            s3_wait_vm<0>();
+            xflush = false;
             return;
         }
         const int y = st_prev + st_cur;
@@ -322,9 +361,7 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         S3T_END(0);
         S3T_BEGIN(1);
-#ifndef S3_AB_NOBAR  // timing-only A/B builds (wrong results): no stage barrier
         __builtin_amdgcn_s_barrier();
-#endif
         asm volatile("" ::: "memory");
         S3T_END(1);
         S3T_BEGIN(2);
@@ -351,72 +388,86 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
     auto mf = [&](f32x4& acc, const bf16x8& x, const bf16x8& y) {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, acc, 0, 0, 0);
     };
-    // one 16-row output tile over NK k-steps (nk live): MODE 1 split forward (hi.hi + hi.lo + lo.hi),
-    // MODE 2 split dgrad (hi.B + lo.B).  A fragments of k-step ks at slot + ks KB (hi) and + LO (lo),
-    // read two k-steps ahead.
-    // PC: this GEMM is its stage's first -- the stage's DMA pieces go out beside its MFMAs (piece j
-    // after k-step 2 j of an 8-k-step GEMM; after the last k-step of a shorter one), so the MFMAs
-    // start right after the barrier; every store of the stage follows (the ring-wait accounting)
-    auto gemm = [&](f32x4& acc, const char* slot, const S3Frag* Bh, const S3Frag* Bl, int nk, auto nk_tag, auto mode_tag,
-                    auto pc_tag) {
-        constexpr int NK = decltype(nk_tag)::value;
-        constexpr int MODE = decltype(mode_tag)::value;
+    // per-lane byte offsets of the composite A operands in a pair's fragments (hi at +0, lo at +LO;
+    // fragment lane (row r, group g) holds k positions 8 g .. 8 g + 7 of the pair)
+    // (recomputed from the lane id at each GEMM: four live offsets cost more registers than the VALU)
+    auto oF1 = [&]() -> unsigned { return (threadIdx.x & 31) * 16; };                                 // [hi(2s) | hi(2s)]
+    auto oF2 = [&]() -> unsigned { return (threadIdx.x & 63) * 16 + ((threadIdx.x & 32) ? 0 : LO); };     // [lo(2s) | hi(2s+1)]
+    auto oF3 = [&]() -> unsigned {  // [hi(2s+1) | lo(2s+1)] (dgrad: the second MFMA)
+        return (threadIdx.x & 32) ? LO + (threadIdx.x & 63) * 16 : ((threadIdx.x & 31) + 32) * 16;
+    };
+    auto oD1 = [&]() -> unsigned { return (threadIdx.x & 31) * 16 + ((threadIdx.x & 32) ? LO : 0); };  // [hi(2s) | lo(2s)]
+
+    // forward: one 16-row output tile over NP operand pairs (np live; the last layer-0 pair of an odd
+    // chunk count has no second chunk: its third MFMA is skipped).  The A fragments of pair s + 1 are
+    // read as pair s's MFMAs go out.  PC: this GEMM is its stage's first -- the stage's DMA pieces go
+    // out beside its MFMAs (piece j after pair 2 j of an 8-pair GEMM; after a shorter one's last pair)
+    auto gemm_f = [&](f32x4& acc, const char* slot, const S3Frag* B1, const S3Frag* B3, int np, auto np_tag,
+                      auto pc_tag) {
+        constexpr int NP = decltype(np_tag)::value;
         constexpr bool PC = decltype(pc_tag)::value;
-        const bf16x8* ah = reinterpret_cast<const bf16x8*>(slot + lane * 16);
-        const bf16x8* al = reinterpret_cast<const bf16x8*>(slot + LO + lane * 16);
-        bf16x8 A0[2], A1[2];
-        A0[0] = ah[0];
-        A1[0] = al[0];
-        if constexpr (NK > 1) {
-            A0[1] = ah[64];
-            A1[1] = al[64];
-        }
-        // sched_barrier pins the order: left alone the scheduler sinks each LDS read to right before
-        // its MFMA (an lgkmcnt(0) wait per MFMA) to save the ring's registers
+        const char* p1 = slot + oF1();
+        const char* p2 = slot + oF2();
+        const char* p3 = slot + oF3();
+        bf16x8 F0 = *reinterpret_cast<const bf16x8*>(p1);
+        bf16x8 F1 = *reinterpret_cast<const bf16x8*>(p2);
+        bf16x8 F2 = *reinterpret_cast<const bf16x8*>(p3);
         __builtin_amdgcn_sched_barrier(0);
-        s3_sfor<NK>([&](auto ksc) {
-            constexpr int ks = decltype(ksc)::value;
-            constexpr int u = ks & 1;
-            const bool live = NK != NK0 || ks < nk;
+        s3_sfor<NP>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            const bool live = NP != NP0 || s < np;
             if (live) {
-                if constexpr (MODE == 1) {
-                    mf(acc, A0[u], Bh[ks].f);
-                    mf(acc, A0[u], Bl[ks].f);
-                    __builtin_amdgcn_sched_barrier(0);
-                    if constexpr (ks + 2 < NK) A0[u] = ah[(ks + 2) * 64];
-                    mf(acc, A1[u], Bh[ks].f);
-                } else {
-                    mf(acc, A0[u], Bh[ks].f);
-                    __builtin_amdgcn_sched_barrier(0);
-                    if constexpr (ks + 2 < NK) A0[u] = ah[(ks + 2) * 64];
-                    mf(acc, A1[u], Bh[ks].f);
-                }
-            } else if constexpr (ks + 2 < NK) {
-                A0[u] = ah[(ks + 2) * 64];
+                S3Frag mid;
+                mid.u = s3_mid(B1[s], B3[s]);
+                mf(acc, F0, B1[s].f);
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (s + 1 < NP) if (NP != NP0 || s + 1 < np) F0 = *reinterpret_cast<const bf16x8*>(p1 + (s + 1) * 1024);
+                mf(acc, F1, mid.f);
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (s + 1 < NP) if (NP != NP0 || s + 1 < np) F1 = *reinterpret_cast<const bf16x8*>(p2 + (s + 1) * 1024);
+                if (!(NP == NP0 && odd_tail && s == np - 1)) mf(acc, F2, B3[s].f);
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (s + 1 < NP) if (NP != NP0 || s + 1 < np) F2 = *reinterpret_cast<const bf16x8*>(p3 + (s + 1) * 1024);
             }
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (ks + 2 < NK) A1[u] = al[(ks + 2) * 64];
-            if constexpr (PC && NK == NKH && (ks & 1) == 0) dma_piece(std::integral_constant<int, ks / 2>());
+            if constexpr (PC && NP == NPH && (s & 1) == 0) dma_piece(std::integral_constant<int, s / 2>());
             __builtin_amdgcn_sched_barrier(0);
         });
-        if constexpr (PC && NK != NKH) dma_burst();
+        if constexpr (PC && NP != NPH) dma_burst();
+    };
+    // dgrad: one 16-row output tile over NP operand pairs: [hd(2s) | ld(2s)], [hd(2s+1) | ld(2s+1)]
+    auto gemm_b = [&](f32x4& acc, const char* slot, const S3Frag* D1, const S3Frag* D2, auto np_tag, auto pc_tag) {
+        constexpr int NP = decltype(np_tag)::value;
+        constexpr bool PC = decltype(pc_tag)::value;
+        const char* q1 = slot + oD1();
+        const char* q2 = slot + oF3();
+        bf16x8 G0 = *reinterpret_cast<const bf16x8*>(q1);
+        bf16x8 G1 = *reinterpret_cast<const bf16x8*>(q2);
+        __builtin_amdgcn_sched_barrier(0);
+        s3_sfor<NP>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            mf(acc, G0, D1[s].f);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (s + 1 < NP) G0 = *reinterpret_cast<const bf16x8*>(q1 + (s + 1) * 1024);
+            mf(acc, G1, D2[s].f);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (s + 1 < NP) G1 = *reinterpret_cast<const bf16x8*>(q2 + (s + 1) * 1024);
+            if constexpr (PC && NP == NPH && (s & 1) == 0) dma_piece(std::integral_constant<int, s / 2>());
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        if constexpr (PC && NP != NPH) dma_burst();
     };
     typedef std::integral_constant<bool, true> PcOn;
     typedef std::integral_constant<bool, false> PcOff;
-    typedef std::integral_constant<int, 1> MFt;
-    typedef std::integral_constant<int, 2> MBt;
-    typedef std::integral_constant<int, NKH> NKHt;
-    typedef std::integral_constant<int, NK0> NK0t;
-    typedef std::integral_constant<int, 1> NK1t;
+    typedef std::integral_constant<int, NPH> NPHt;
+    typedef std::integral_constant<int, NP0> NP0t;
 
     auto bias_init = [&](int boff, int rt) -> f32x4 {
         const float4 v = *reinterpret_cast<const float4*>(bias_l + boff + rt * 16 + 4 * grp);
         return (f32x4){v.x, v.y, v.z, v.w};
     };
-    // a packed k-step (x, y: features 32 s + 4 g + 0..3 of the lane's pixel; z, w: 32 s + 16 + 4 g + 0..3)
-    // into a natural-order [S][ld] bf16 row: one v_permlane16_swap per dword pair puts features
-    // 32 s + 16 (g & 1) + 8 (g >> 1) + 0..7 in every lane: one 16-B store
-    //  (row = the lane's row base + 16 (g & 1) + 8 (g >> 1) elements; k-step S at instruction offset 64 S)
+    // an operand pair's hi words (lane group g: features F(s, g, 0..7)) into a natural-order [S][ld]
+    // bf16 row: one v_permlane16_swap per dword pair gives lane group g features 32 s + 8 g + 0..7:
+    // one 16-B store at the row base + 8 g elements, pair S at instruction offset 64 S
     auto store_ks = [&](u16* row, auto sc, const uint4& u) {
         constexpr int S = decltype(sc)::value;
         const auto xz = __builtin_amdgcn_permlane16_swap(u.x, u.z, false, false);
@@ -424,23 +475,47 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
         s3_st16o<64 * S>(row, make_uint4(xz[0], yw[0], xz[1], yw[1]));
         st_cur += 1;
     };
-    const int colg = 16 * (grp & 1) + 8 * (grp >> 1);
+    const int colg = 8 * grp;
 
-    S3Frag Bh[NKH], Bl[NKH], Oh[NKH], Ol[NKH];
+    S3Frag Bh[NPH], Bl[NPH], Oh[NPH], Ol[NPH];
     const float pi_f = 3.14159265358979323846f;
 
+    // ---- the pair's dH partial: both waves leave their pixels' 9 terms in the pair buffer at the end
+    //      of a tile; the first-half wave reduces the 32 pixels with k_step2's DPP tree after the next
+    //      barrier (or after the loop) and stores k_step2's per-32-pixel partial
+    long long dh_pending = -1;  // (first half) the pending partial's index
+    auto flush_dH = [&]() {
+        const float* pd = reinterpret_cast<const float*>(pbuf + PB_DH);
+        float mine = 0.f;
+#pragma unroll
+        for (int e = 0; e < 9; ++e) {
+            const float v = lo32 ? pd[e * 32 + lane] : 0.f;
+            const float sm = wave_total63(v);
+            const float sb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm), 63));
+            if (lane == e) mine = sb;
+        }
+        s3_st4(lane < 9 ? (void*)(a.dH_partial + (size_t)dh_pending * 9 + lane) : (void*)dmy, mine);
+        st_cur += 1;
+        dh_pending = -1;
+    };
+
+#ifdef S3_SETPRIO
+    if (half) __builtin_amdgcn_s_setprio(1);
+#endif
     S3T_BEGIN(15);
     for (int ti = 0; ti < my_tiles; ++ti) {
         S3T_BEGIN(3);
         const int tile = tbase + ti * (int)gridDim.x;
         const int pb = ti & 1;
         const int b = tile / tpp;
-        const int p0 = (tile - b * tpp) * TPX + PX * wave;
+        const int q0 = (tile - b * tpp) * TPX;
+        const int p0 = q0 + PX * pblk;
         const long long slot0 = (long long)b * a.geo.Np_pad + p0;
         const long long myslot = slot0 + pxl;
         const int p = p0 + pxl;
         const bool valid = p < Np;
         const float* pro = pro_buf(pb);
+        const int pix = PX * pblk + pxl;  // pixel within the block tile
 
         // ---- prologue: pixel grid -> warp (warp.py:33-81) -> posenc + c2f (model/planar.py:451-471)
         float u, v, X[3];
@@ -458,65 +533,53 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
             warp_point(pro + 4 * TPX, x, y, u, v, X, a.geo.bmm_small);
         }
         {
-            // layer-0 operand: band k-step ks, group g: bands 8 ks + 4 (g >> 1) + 0..3 of coordinate
-            // g & 1, sin (j < 4) then cos; k-step nb: the raw coordinates (group 0: u, 1: v)
+            // layer-0 operand pair s, lane group g: k_step2's chunk c = 2 s + (g >> 1) of coordinate
+            // g & 1: c < ng: bands 4 c + 0..3, sin then cos; c = ng: the raw coordinate; beyond: zero
             const float cd = (grp & 1) ? v : u;
+            u16* row = (!a.fwd_only && !a.feat0_recompute) ? ly_ptr(0, 0) + myslot * ly_int(0, 3) : nullptr;
+            const int ldf0 = row ? ly_int(0, 3) : 0;
+            s3_sfor<NP0>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                if (s < np0) {
+                    const int c = 2 * s + (grp >> 1);
+                    float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                    if (c < ng) {
 #pragma unroll
-            for (int ks = 0; ks < NK0 - 1; ++ks) {
-                if (ks < nb) {
-                    float f[8];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int k = 8 * ks + 4 * (grp >> 1) + i;
-                        float sn = 0.f, co = 0.f;
-                        if (k < L) {
-                            band_sincos<true>(cd, k, sn, co);
-                            if (a.c2f_on) {
-                                const float w = c2f_l[k];
-                                sn = sn * w;
-                                co = co * w;
+                        for (int i = 0; i < 4; ++i) {
+                            const int k = 4 * c + i;
+                            float sn = 0.f, co = 0.f;
+                            if (k < L) {
+                                band_sincos<true>(cd, k, sn, co);
+                                if (a.c2f_on) {
+                                    const float w = c2f_l[k];
+                                    sn = sn * w;
+                                    co = co * w;
+                                }
                             }
+                            f[i] = sn;
+                            f[4 + i] = co;
                         }
-                        f[i] = sn;
-                        f[4 + i] = co;
+                    } else if (c == ng) {
+                        f[0] = cd;
                     }
-                    s3_split8(f, Bh[ks], Bl[ks]);
-                }
-            }
-            float f[8] = {grp == 0 ? u : (grp == 1 ? v : 0.f), 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            S3Frag rh, rl;
-            s3_split8(f, rh, rl);
-#pragma unroll
-            for (int ks = 0; ks < NK0; ++ks)
-                if (ks == nb) {
-                    Bh[ks] = rh;
-                    Bl[ks] = rl;
-                }
-            // feat_0 (bf16 hi) in k_step2's column order, which the layer-0 weight gradient and its
-            // column map read: band group q (4 bands, sin then cos) of coordinate h at column
-            // 16 q + 8 h, the raw coordinates in group ng, zero columns up to ldf0
-            if (!a.fwd_only && !a.feat0_recompute) {
-                u16* row = ly_ptr(0, 0) + myslot * ly_int(0, 3);
-                const int ng = (L + 3) / 4, ldf0 = ly_int(0, 3);
-#pragma unroll
-                for (int ks = 0; ks < NK0 - 1; ++ks) {
-                    if (ks < nb) {
-                        const int q = 2 * ks + (grp >> 1);
-                        s3_st16(q < ng ? (void*)(row + 16 * q + 8 * (grp & 1)) : (void*)dmy, Bh[ks].u);
+                    uint4 H, Lw;
+                    s3_split8(f, H, Lw);
+                    // feat_0 (bf16 hi) in k_step2's column order: chunk c of coordinate h at column
+                    // 16 c + 8 h, zero columns up to ldf0
+                    if (row) {
+                        const bool st = c <= ng || 16 * c + 8 * (grp & 1) < ldf0;
+                        s3_st16(st ? (void*)(row + 16 * c + 8 * (grp & 1)) : (void*)dmy, H);
                         st_cur += 1;
                     }
+                    s3_fwd_pair(H, Lw, lo32, Bh[s], Bl[s]);
                 }
-                const bool raw = grp < 2, pad = grp >= 2 && 16 * (ng + 1) + 8 * (grp & 1) < ldf0;
-                s3_st16(raw ? (void*)(row + 16 * ng + 8 * grp) : (pad ? (void*)(row + 16 * (ng + 1) + 8 * (grp & 1)) : (void*)dmy),
-                        raw ? rh.u : make_uint4(0, 0, 0, 0));
-                st_cur += 1;
-            }
+            });
         }
 
         // ---- forward: layer 0, hidden layers.  Row tile rt of layer l: acc = bias + W . B, epilogue,
-        //      the pair (2s, 2s + 1) -> operand k-step s of layer l + 1 (+ feat_{l+1} store, mask words)
-        auto fwd_layer = [&](int l, const S3Frag* BH, const S3Frag* BL, int nk, auto nk_tag, int r0) {
-            const int nrt = FULL ? (l == 0 ? NRT : NRT) : ly_int(l, 0);
+        //      the pair (2s, 2s + 1) -> operand pair s of layer l + 1 (+ feat_{l+1} store, mask words)
+        auto fwd_layer = [&](int l, int np, auto np_tag, int r0) {
+            const int nrt = FULL ? NRT : ly_int(l, 0);
             const bool save = l + 1 < nl - 1 && !a.fwd_only;
             u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) + colg : nullptr;
             const int boff = ly_int(l, 2);
@@ -530,26 +593,29 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
                     const int sub = rt % r0;
                     if (sub == 0) {
                         slot = stage_begin();
-                        // the next tile's target / mask / H into the other input buffer
-                        if (l == 0 && rt == 0 && ti + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
+                        if (l == 0 && rt == 0) {
+                            // the next tile's target / mask / H into the other input buffer; the
+                            // previous tile's dH partial (its terms are in the pair buffer)
+                            if (ti + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
+                            if (half == 0 && dh_pending >= 0) flush_dH();
+                        }
                     }
                     f32x4 acc = bias_init(boff, rt);
                     S3T_BEGIN(6);
                     if (sub == 0)
-                        gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt(), PcOn());
+                        gemm_f(acc, slot + sub * np * 1024, Bh, Bl, np, np_tag, PcOn());
                     else
-                        gemm(acc, slot + sub * nk * 1024, BH, BL, nk, nk_tag, MFt(), PcOff());
+                        gemm_f(acc, slot + sub * np * 1024, Bh, Bl, np, np_tag, PcOff());
                     S3T_END(6);
                     S3T_BEGIN(7);
                     const S3Ep e = s3_fwd_ep(acc);
-                    // the lo words computed here, not deferred to the layer's end, where the compiler
-                    // would keep the 64 fp32 values alive (26 registers)
                     asm volatile("" ::"v"(e.l0), "v"(e.l1));
                     mword = (mword << 2) | e.nib;
                     if constexpr (rt & 1) {
-                        Oh[rt >> 1].u = make_uint4(ev.h0, ev.h1, e.h0, e.h1);
-                        Ol[rt >> 1].u = make_uint4(ev.l0, ev.l1, e.l0, e.l1);
-                        if (save) store_ks(srow, std::integral_constant<int, (rt >> 1)>(), Oh[rt >> 1].u);
+                        const uint4 H = make_uint4(ev.h0, ev.h1, e.h0, e.h1);
+                        const uint4 Lw = make_uint4(ev.l0, ev.l1, e.l0, e.l1);
+                        if (save) store_ks(srow, std::integral_constant<int, (rt >> 1)>(), H);
+                        s3_fwd_pair(H, Lw, lo32, Oh[rt >> 1], Ol[rt >> 1]);
                     } else {
                         ev = e;
                     }
@@ -563,17 +629,17 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
                 }
             });
 #pragma unroll
-            for (int k = 0; k < NKH; ++k) {
+            for (int k = 0; k < NPH; ++k) {
                 Bh[k] = Oh[k];
                 Bl[k] = Ol[k];
             }
         };
         S3T_END(3);
         S3T_BEGIN(4);
-        fwd_layer(0, Bh, Bl, nk0, NK0t(), FULL ? R0F : a.r0);
+        fwd_layer(0, np0, NP0t(), FULL ? R0F : a.r0);
         S3T_END(4);
         S3T_BEGIN(5);
-        for (int l = 1; l < nl - 1; ++l) fwd_layer(l, Bh, Bl, NKH, NKHt(), 2);
+        for (int l = 1; l < nl - 1; ++l) fwd_layer(l, NPH, NPHt(), 2);
         S3T_END(5);
         S3T_BEGIN(8);
 
@@ -582,18 +648,18 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
         {
             f32x4 acc = bias_init(ly_int(nl - 1, 2), 0);
             const char* slot = stage_begin();
-            gemm(acc, slot, Bh, Bl, NKH, NKHt(), MFt(), PcOn());
+            gemm_f(acc, slot, Bh, Bl, NPH, NPHt(), PcOn());
             float* o = (a.rgb && valid && grp == 0) ? a.rgb + ((size_t)b * Np + p) * 3 : dmy;
             float yv[3] = {0.f, 0.f, 0.f};
             if (grp == 0) {
-                const float m = valid ? (a.mask ? pro[3 * TPX + PX * wave + pxl] : 1.0f) : 0.f;
+                const float m = valid ? (a.mask ? pro[3 * TPX + pix] : 1.0f) : 0.f;
                 float sqf = 0.f;
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     const float z = acc[c];
                     const float yy = 1.0f / (1.0f + expf(-z));
                     yv[c] = yy;
-                    const float tg = valid ? pro[c * TPX + PX * wave + pxl] : 0.f;
+                    const float tg = valid ? pro[c * TPX + pix] : 0.f;
                     // model/planar.py:388-390 and its autograd: x = (p - g) m, d = 2 x m
                     const float xx = (yy - tg) * m;
                     sqf += xx * xx;
@@ -613,68 +679,94 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
         if (a.fwd_only) continue;
 
         S3T_BEGIN(9);
-        // g as a split pair: hi = bf16(g), lo = bf16(g - hi)
+        // g as a split pair: hi = bf16(g), lo = bf16(g - hi) (k_step2's Bg)
         float ghi[3], glo[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             ghi[c] = s3_lo16(s3_pk(g[c], 0.f));
             glo[c] = g[c] - ghi[c];
         }
-        // ---- last-layer weight gradient of the wave's 16 pixels: dW[c][k] += sum_px g[c] feat[k]
-        //      (feat = the last layer's input, bf16 hi).  v_mfma_f32_16x16x32_bf16 with A = g^T (rows
-        //      c, k = pixels 0..15; 16..31 zero) hi and lo, B = feat^T per 16 features through a
-        //      transposing LDS round trip (ds_read_b64_tr_b16)
+        // ---- last-layer weight gradient, k_step2's chain: per 16 features one 16x16x32 MFMA with
+        //      A = g^T (rows 0-2 hi, 4-6 lo; k = the 32 pixels of the pair), B = feat^T (the last layer's
+        //      input, bf16 hi, through a transposing LDS round trip); the first-half wave runs pixels
+        //      0..15 from 0, the second-half wave pixels 16..31 from that partial, then
+        //      dW[c][f] += (row c) + (row 4 + c)
+        if (grp == 0) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                gimg[c * 16 + pxl] = (u16)(s3_pk(ghi[c], 0.f) & 0xffff);
+                gimg[(4 + c) * 16 + pxl] = (u16)(s3_pk(glo[c], 0.f) & 0xffff);
+            }
+        }
+        asm volatile("" ::: "memory");
+        S3Frag ga;  // A: this wave's half of k (lane groups 2 half, 2 half + 1), zero elsewhere
         {
-            if (grp == 0) {
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    gimg[c * 16 + pxl] = (u16)(s3_pk(ghi[c], 0.f) & 0xffff);
-                    gimg[(3 + c) * 16 + pxl] = (u16)(s3_pk(glo[c], 0.f) & 0xffff);
-                }
-            }
-            asm volatile("" ::: "memory");
             const int rc = lane & 15, kg = lane >> 4;
-            S3Frag gah, gal;
-            gah.u = gal.u = make_uint4(0, 0, 0, 0);
-            {
-                const uint4 th = *reinterpret_cast<const uint4*>(gimg + min(rc, 2) * 16 + 8 * (kg & 1));
-                const uint4 tl = *reinterpret_cast<const uint4*>(gimg + (3 + min(rc, 2)) * 16 + 8 * (kg & 1));
-                if (rc < 3 && kg < 2) {
-                    gah.u = th;
-                    gal.u = tl;
-                }
-            }
-            const int q = (lane & 15) >> 2, pq = lane & 3;
-            const int nkl = a.Kl / 32;
+            const uint4 t = *reinterpret_cast<const uint4*>(gimg + (rc & 7) * 16 + 8 * (kg & 1));
+            ga.u = ((kg >> 1) == half && rc < 8 && (rc & 3) < 3) ? t : make_uint4(0, 0, 0, 0);
+        }
+        float* const xb = a.xbuf + (((size_t)blockIdx.x * 4 + W) * XQ) * 128 + (lane & 31) * 4;  // [q][32 lanes][4]
+        auto dw_last = [&](float* xv) {  // xv: the pair's partial (second half: in; first half: 12-float staging)
+            const int q = (lane & 15) >> 2, pq = lane & 3, kg = lane >> 4;
+            s3_sfor<NPH>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                __builtin_amdgcn_sched_barrier(0);  // one pair at a time (the scheduler would hoist every read)
+                const uint4 hv = s3_mid(Bh[s], Bl[s]);
+                asm volatile("" ::: "memory");
+                uint2* w2 = reinterpret_cast<uint2*>(scr + pxl * 32);  // natural feature order of the pair
+                w2[4 * (grp >> 1) + (grp & 1)] = make_uint2(hv.x, hv.y);
+                w2[4 * (grp >> 1) + 2 + (grp & 1)] = make_uint2(hv.z, hv.w);
+                asm volatile("" ::: "memory");
 #pragma unroll
-            for (int s = 0; s < NKH; ++s) {
-                if (s < nkl) {
-                    asm volatile("" ::: "memory");
-                    uint2* w2 = reinterpret_cast<uint2*>(scr + pxl * 32);
-                    w2[grp] = make_uint2(Bh[s].u.x, Bh[s].u.y);      // features 4 g + 0..3
-                    w2[4 + grp] = make_uint2(Bh[s].u.z, Bh[s].u.w);  // features 16 + 4 g + 0..3
-                    asm volatile("" ::: "memory");
+                for (int fb = 0; fb < 2; ++fb) {
+                    const u16* b0 = scr + (8 * (kg & 1) + q) * 32 + 16 * fb + 4 * pq;
+                    i16x4 vv[2] = {s3_tr16(b0), s3_tr16(b0 + 4 * 32)};
+                    const bf16x8 bt = *reinterpret_cast<bf16x8*>(vv);
+                    const int m = 2 * s + fb;
+                    if (half == 0) {
+                        // rows 0..2 of lanes 0..31 (hi rows of group 0, lo rows of group 1): 3 floats per
+                        // MFMA, stored 16 B per lane every 4 MFMAs
+                        const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga.f, bt, (f32x4){}, 0, 0, 0);
+                        const int mm = m & 3;
+                        xv[3 * mm] = d[0];
+                        xv[3 * mm + 1] = d[1];
+                        xv[3 * mm + 2] = d[2];
+                        if (mm == 3) {
 #pragma unroll
-                    for (int fb = 0; fb < 2; ++fb) {
-                        const u16* b0 = scr + (8 * (kg & 1) + q) * 32 + 16 * fb + 4 * pq;
-                        i16x4 vv[2] = {s3_tr16(b0), s3_tr16(b0 + 4 * 32)};
-                        const bf16x8 bt = *reinterpret_cast<bf16x8*>(vv);
-                        f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gah.f, bt, (f32x4){}, 0, 0, 0);
-                        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gal.f, bt, d, 0, 0, 0);
-                        if (lane < 16) {
+                            for (int k = 0; k < 3; ++k) {
+                                const int qd = 3 * (m >> 2) + k;
+                                s3_st16(lo32 ? (void*)(xb + qd * 128) : (void*)dmy,
+                                        make_uint4(__float_as_uint(xv[4 * k]), __float_as_uint(xv[4 * k + 1]),
+                                                   __float_as_uint(xv[4 * k + 2]), __float_as_uint(xv[4 * k + 3])));
+                            }
+                        }
+                    } else {
+                        const f32x4 x0 = lo32 ? (f32x4){xv[3 * m], xv[3 * m + 1], xv[3 * m + 2], 0.f} : (f32x4){};
+                        const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga.f, bt, x0, 0, 0, 0);
+                        float lo[3];
 #pragma unroll
-                            for (int c = 0; c < 3; ++c) wla[c * a.Kl + 32 * s + 16 * fb + lane] += d[c];
+                        for (int c = 0; c < 3; ++c) lo[c] = __shfl_down(d[c], 16, 64);
+                        if (lane < 16 && 32 * s < a.Kl) {  // (a narrower last-layer input: zero pairs past Kl)
+#pragma unroll
+                            for (int c = 0; c < 3; ++c) wla[c * a.Kl + 32 * s + 16 * fb + lane] += d[c] + lo[c];
                         }
                     }
                 }
-            }
+            });
+        };
+        if (half == 0) {
+            float xv[12];
+            dw_last(xv);
+            st_cur += XQ;
+            xflush = true;  // the partner loads them after the next barrier
         }
 
         S3T_END(9);
         S3T_BEGIN(10);
-        // ---- last-layer dgrad: dfeat = W_{n-1}^T g (one k-step per row tile: lanes 0..15 carry
-        //      k = [g hi (3), 0, g lo (3), 0]), mask -> dz_{n-1}; one stage holds every row tile
-        S3Frag gB;
+        // ---- last-layer dgrad: dfeat = W_{n-1}^T g as ONE MFMA per row tile, [hd | ld] with B = [gB | gB]
+        //      (lane group 0: k = [g hi (3), 0, g lo (3), 0], k_step2's Bg), mask -> dz_{n-1}; one
+        //      stage holds every row tile's fragments (tile rt at rt KB)
+        S3Frag gB1;
         {
             float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             if (grp == 0) {
@@ -684,7 +776,11 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
                     f[4 + c] = glo[c];
                 }
             }
-            gB.u = make_uint4(s3_pk(f[0], f[1]), s3_pk(f[2], f[3]), s3_pk(f[4], f[5]), s3_pk(f[6], f[7]));
+            const uint32_t w[4] = {s3_pk(f[0], f[1]), s3_pk(f[2], f[3]), s3_pk(f[4], f[5]), s3_pk(f[6], f[7])};
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = __builtin_amdgcn_permlane32_swap(w[q], w[q], false, false)[0];
+            gB1.u = make_uint4(o[0], o[1], o[2], o[3]);
         }
         auto bwd_pass = [&](int l, int lmask, int nrt, const char* slot_first, bool last) {
             // row tiles of dz: last: every tile from one stage (tile rt at rt KB); else two per stage
@@ -699,52 +795,68 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
                     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
                     if (last) {
                         S3T_BEGIN(11);
-                        if constexpr (rt == 0)
-                            gemm(acc, slot + rt * 1024, &gB, &gB, 1, NK1t(), MBt(), PcOn());
-                        else
-                            gemm(acc, slot + rt * 1024, &gB, &gB, 1, NK1t(), MBt(), PcOff());
+                        const bf16x8 A = *reinterpret_cast<const bf16x8*>(slot + rt * 1024 + oD1());
+                        mf(acc, A, gB1.f);
+                        if constexpr (rt == 0) dma_burst();
                         S3T_END(11);
                     } else {
                         if constexpr ((rt & 1) == 0) slot = stage_begin();
                         S3T_BEGIN(11);
-                        gemm(acc, slot + (rt & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt(),
-                             std::integral_constant<bool, (rt & 1) == 0>());
+                        gemm_b(acc, slot + (rt & 1) * NPH * 1024, Bh, Bl, NPHt(),
+                               std::integral_constant<bool, (rt & 1) == 0>());
                         S3T_END(11);
                     }
                     S3T_BEGIN(12);
                     const uint2 hw = s3_bwd_ep<2 * (7 - (rt & 7))>(acc, mw);
                     if constexpr (rt & 1) {
-                        Oh[rt >> 1].u = make_uint4(hv0, hv1, hw.x, hw.y);
-                        store_ks(brow, std::integral_constant<int, (rt >> 1)>(), Oh[rt >> 1].u);
+                        const uint4 H = make_uint4(hv0, hv1, hw.x, hw.y);
+                        store_ks(brow, std::integral_constant<int, (rt >> 1)>(), H);
+                        s3_bwd_pair(H, Oh[rt >> 1], Ol[rt >> 1]);
                     } else {
                         hv0 = hw.x;
                         hv1 = hw.y;
                     }
                     S3T_END(12);
                 } else if constexpr ((rt & 1) == 0) {
-                    Oh[rt >> 1].u = make_uint4(0, 0, 0, 0);
+                    Oh[rt >> 1].u = Ol[rt >> 1].u = make_uint4(0, 0, 0, 0);
                 }
             });
 #pragma unroll
-            for (int k = 0; k < NKH; ++k) Bh[k] = Oh[k];
+            for (int k = 0; k < NPH; ++k) {
+                Bh[k] = Oh[k];
+                Bl[k] = Ol[k];
+            }
         };
         {
             const char* slot = stage_begin();
+            if (half == 1) {  // the second half of the pair's dW_last chain, from the partner's partial
+                float xv[3 * 2 * NPH];
+                typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+                for (int qd = 0; qd < XQ; ++qd) {
+                    const u32x4v t = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(xb + qd * 128));
+                    xv[4 * qd] = __uint_as_float(t[0]);
+                    xv[4 * qd + 1] = __uint_as_float(t[1]);
+                    xv[4 * qd + 2] = __uint_as_float(t[2]);
+                    xv[4 * qd + 3] = __uint_as_float(t[3]);
+                }
+                dw_last(xv);
+            }
             bwd_pass(nl - 1, nl - 2, FULL ? NRT : ly_int(nl - 1, 1), slot, true);
         }
         for (int l = nl - 2; l >= 1; --l) bwd_pass(l, l - 1, FULL ? NRT : ly_int(l, 1), nullptr, false);
         S3T_END(10);
         S3T_BEGIN(13);
 
-        // ---- layer-0 dgrad + posenc adjoint: row tile t, register r of lane group G holds band
-        //      4 t + r of coordinate G >> 1, the sin slot for even G, the cos slot for odd G (the raw
-        //      coordinates: tile 2 nb, register 0 of groups 0 (u) and 2 (v)).  One v_permlane16_swap
-        //      gives each lane its partner group's slot of the same band, so every lane forms the
-        //      band's term as k_step2 and torch's autograd of sin / cos do, (g_sin cos - g_cos sin)
-        //      2^k pi, accumulated over the bands in increasing k, then the raw coordinate
+        // ---- layer-0 dgrad + posenc adjoint: row tile t < ng, register r of lane group G holds band
+        //      4 t + r of coordinate G >> 1, the sin slot for even G, the cos slot for odd G; tile ng
+        //      the raw coordinates (register 0 of groups 0 (u) and 2 (v)).  One v_permlane16_swap gives
+        //      each lane its partner group's slot of the same band, so every lane forms the band's term
+        //      as k_step2 and torch's autograd of sin / cos do, (g_sin cos - g_cos sin) 2^k pi,
+        //      accumulated over the bands in increasing k, then the raw coordinate
         float dc = 0.f;
         {
-            const int nta = FULL ? NTA : a.nta;
+            const int nta = FULL ? ng + 1 : a.nta;
             const float cd = (grp >> 1) ? v : u;
             const bool sinl = (grp & 1) == 0;
             const char* slot = nullptr;
@@ -753,8 +865,8 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
                 if (t < nta) {
                     if constexpr ((t & 1) == 0) slot = stage_begin();
                     f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-                    gemm(acc, slot + (t & 1) * NKH * 1024, Bh, Bh, NKH, NKHt(), MBt(), std::integral_constant<bool, (t & 1) == 0>());
-                    if (t < 2 * nb) {
+                    gemm_b(acc, slot + (t & 1) * NPH * 1024, Bh, Bl, NPHt(), std::integral_constant<bool, (t & 1) == 0>());
+                    if (t < ng) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int k = 4 * t + r;
@@ -773,7 +885,7 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
                                 dc += (gs * co - gc * sn) * ldexpf(pi_f, k);
                             }
                         }
-                    } else if (t == 2 * nb) {
+                    } else if (t == ng) {
                         dc += acc[0];  // (read from groups 0 and 2 only)
                     }
                 }
@@ -781,7 +893,7 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
         }
         S3T_END(13);
         S3T_BEGIN(14);
-        // ---- (u, v) = X[:2] / (X[2] + 1e-8) backward, the bmm backward -> dH partial of the wave
+        // ---- (u, v) = X[:2] / (X[2] + 1e-8) backward, the bmm backward -> the pixel's dH terms
         {
             const float du = dc, dv = __shfl(dc, (lane & 15) + 32, 64);  // groups 0: du, 2: dv
             float h9[9];
@@ -803,15 +915,12 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
                     h9[6 + c] = dX2 * hom[c];
                 }
             }
-            float mine = 0.f;
+            if (grp == 0) {
+                float* pd = reinterpret_cast<float*>(pbuf + PB_DH);
 #pragma unroll
-            for (int e = 0; e < 9; ++e) {
-                const float sm = wave_total63(h9[e]);
-                const float sb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm), 63));
-                if (lane == e) mine = sb;
+                for (int e = 0; e < 9; ++e) pd[e * 32 + 16 * half + pxl] = h9[e];
             }
-            s3_st4(lane < 9 ? (void*)(a.dH_partial + (size_t)(slot0 / PX) * 9 + lane) : (void*)dmy, mine);
-            st_cur += 1;
+            if (half == 0) dh_pending = ((long long)b * a.geo.Np_pad + q0 + 32 * W) / 32;
         }
         S3T_END(14);
     }
@@ -821,26 +930,40 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
         for (int k = 0; k < 16; ++k) a.stamps[(size_t)blockIdx.x * 16 + k] = tacc[k];
 #endif
 
-    // ---- per-block partials (fixed order over waves)
+    // ---- per-block partials (fixed order over k_step2's waves W = 0..3)
     s3_wait_vm<0>();
     __syncthreads();
+    if (half == 0 && dh_pending >= 0) flush_dH();
+    if (grp == 0) {
+        reinterpret_cast<double*>(pbuf + PB_LSQ)[16 * half + pxl] = lsq;
+        reinterpret_cast<double*>(pbuf + PB_LMS)[16 * half + pxl] = lms;
+        float* pl = reinterpret_cast<float*>(pbuf + PB_BL);
+        pl[16 * half + pxl] = bl0;
+        pl[32 + 16 * half + pxl] = bl1;
+        pl[64 + 16 * half + pxl] = bl2;
+    }
+    __syncthreads();
     double* red = reinterpret_cast<double*>(smem);  // the ring is idle now
-    {
-        const double s0 = wave_total63(lsq), s1 = wave_total63(lms);
-        const float t0 = wave_total63(bl0), t1 = wave_total63(bl1), t2 = wave_total63(bl2);
+    if (half == 0) {
+        const double* pl2 = reinterpret_cast<const double*>(pbuf + PB_LSQ);
+        const double* pm2 = reinterpret_cast<const double*>(pbuf + PB_LMS);
+        const float* pl = reinterpret_cast<const float*>(pbuf + PB_BL);
+        const double s0 = wave_total63(lo32 ? pl2[lane] : 0.0), s1 = wave_total63(lo32 ? pm2[lane] : 0.0);
+        const float t0 = wave_total63(lo32 ? pl[lane] : 0.f), t1 = wave_total63(lo32 ? pl[32 + lane] : 0.f);
+        const float t2 = wave_total63(lo32 ? pl[64 + lane] : 0.f);
         if (lane == 63) {
-            red[wave * 5 + 0] = s0;
-            red[wave * 5 + 1] = s1;
-            red[wave * 5 + 2] = (double)t0;
-            red[wave * 5 + 3] = (double)t1;
-            red[wave * 5 + 4] = (double)t2;
+            red[W * 5 + 0] = s0;
+            red[W * 5 + 1] = s1;
+            red[W * 5 + 2] = (double)t0;
+            red[W * 5 + 3] = (double)t1;
+            red[W * 5 + 4] = (double)t2;
         }
     }
     __syncthreads();
     if (threadIdx.x < 5) {
         double s = 0.0;
         float sf = 0.f;
-        for (int w = 0; w < NW; ++w) {
+        for (int w = 0; w < 4; ++w) {
             s += red[w * 5 + threadIdx.x];
             sf += (float)red[w * 5 + threadIdx.x];
         }
@@ -849,41 +972,56 @@ __global__ __launch_bounds__(64 * NWT, NWT / 4) void k_step3(Step2Args a) {
     }
     for (int e = threadIdx.x; e < 3 * a.Kl; e += NW * 64) {
         float s = 0.f;
-        for (int w = 0; w < NW; ++w) s += reinterpret_cast<const float*>(smem + a.lds_wave + w * a.lds_wave_bytes + W_WLA)[e];
+        for (int w = 0; w < 4; ++w)
+            s += reinterpret_cast<const float*>(smem + a.lds_wave + (w + 4) * a.lds_wave_bytes + W_WLA)[e];
         a.wlast_partial[(size_t)blockIdx.x * 3 * a.Kl + e] = s;
     }
 }
 
 // ------------------------------------------------------------------ weight program packing
 
-// layer-0 operand k index (k-step ks, group g, element j) -> input feature of the reference's
-// [x, y, posenc] vector (model/planar.py:451-471: posenc = [sin bands of x, of y, cos ...] as
-// 2 + 2 h L + (cos ? L : 0) + band); -1: a zero slot
-MARF_DEV int s3_l0_feature(int ks, int g, int j, int L, int nb) {
-    if (ks == nb) return (j == 0 && g < 2) ? g : -1;
-    const int band = 8 * ks + 4 * (g >> 1) + (j & 3);
-    if (band >= L) return -1;
-    return 2 + 2 * (g & 1) * L + (j >= 4 ? L : 0) + band;
+// output feature of row r of 16-row output tile rt (the pair of tiles (2 s, 2 s + 1) packs to operand
+// pair s: lane group g of tile 2 s + b holds features 32 s + 16 (g >> 1) + 8 b + 4 (g & 1) + 0..3)
+MARF_DEV int s3_mrow(int rt, int r) { return 32 * (rt >> 1) + 16 * (r >> 3) + 8 * (rt & 1) + 4 * ((r >> 2) & 1) + (r & 3); }
+// operand pair feature F(s, g, j) = k_step2's s2_kperm(chunk 2 s + (g >> 1), g & 1, j)
+MARF_DEV int s3_kfeat(int s, int g, int j) { return 32 * s + 16 * (g >> 1) + 8 * (j >> 2) + 4 * (g & 1) + (j & 3); }
+// layer-0 operand pair feature of the reference's [x, y, posenc] vector (model/planar.py:451-471:
+// posenc = [sin bands of x, of y, cos ...] at 2 + 2 h L + (cos ? L : 0) + band): k_step2's
+// s2_l0_fwd_feature of chunk 2 s + (g >> 1), coordinate g & 1; -1: a zero slot
+MARF_DEV int s3_l0_feature(int s, int g, int j, int L, int ng) {
+    const int c = 2 * s + (g >> 1), h = g & 1;
+    if (c == ng) return j == 0 ? h : -1;
+    if (c > ng) return -1;
+    const int k = 4 * c + (j & 3);
+    if (k >= L) return -1;
+    return 2 + 2 * h * L + (j >= 4 ? L : 0) + k;
 }
-// hidden operand k index (k-step s, group g, element j) -> feature (the accumulator-pair order)
-MARF_DEV int s3_kperm(int s, int g, int j) { return 32 * s + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4); }
+// layer-0 input feature of adjoint row r of tile t (-1: none)
+MARF_DEV int s3_adj_feature(int t, int r, int L, int ng) {
+    const int G = r >> 2, i = r & 3;
+    if (t == ng) return (i == 0 && (G & 1) == 0) ? (G >> 1) : -1;
+    if (t > ng) return -1;
+    const int k = 4 * t + i;
+    if (k >= L) return -1;
+    return 2 + 2 * (G >> 1) * L + ((G & 1) ? L : 0) + k;
+}
 
 // One thread per (stage, part, fragment, lane, element).  Stage sequence per tile: layer-0 forward
-// (r0 row tiles of nk0 k-steps each), hidden forward (pairs of row tiles), last layer, last-layer
-// dgrad (every row tile's single k-step), hidden dgrad l = nl-2 .. 1 (pairs), adjoint (pairs).
-// A fragment of row tile rt, k-step ks: lane l holds row 16 rt + (l & 15), k index (ks, l >> 4, j).
+// (r0 row tiles of np0 pairs each), hidden forward (pairs of row tiles), last layer, last-layer
+// dgrad (every row tile's fragment), hidden dgrad l = nl-2 .. 1 (pairs), adjoint (pairs).
+// A fragment of row tile rt, pair s: lane l holds row r = l & 15, k positions (s, g = l >> 4, j).
 __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog, float* __restrict__ bias_out,
                         int* __restrict__ kmap, Pack2Args a) {
     const int per_slot = s3::SLOT / 2;
     const long long total = (long long)a.n_stages * per_slot;
     const int D = a.dims[0];
-    const int nb = a.nk0 - 1;
+    const int ng = (a.L + 3) / 4, np0 = a.nk0;
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total + a.nbias + D; e += (long long)gridDim.x * 256) {
         if (e >= total + a.nbias) {
             // layer-0 column map of feat_0 (k_step2's column order): true input feature f -> column
-            const int f = (int)(e - total - a.nbias), L = a.L, ng = (L + 3) / 4;
+            const int f = (int)(e - total - a.nbias), L = a.L, ngc = (L + 3) / 4;
             int col;
-            if (f < 2) col = 16 * ng + 8 * f;
+            if (f < 2) col = 16 * ngc + 8 * f;
             else {
                 const int q = f - 2, hh = q / (2 * L), rr = q - hh * 2 * L, cosp = rr >= L, k = rr - cosp * L;
                 col = 16 * (k / 4) + 8 * hh + 4 * cosp + (k % 4);
@@ -891,13 +1029,15 @@ __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog
             kmap[f] = col;
             continue;
         }
-        if (e >= total) {  // padded bias table
+        if (e >= total) {  // padded bias table, rows in the output tiles' order (s3_mrow)
             const int be = (int)(e - total);
             float v = 0.f;
             for (int l = 0; l < a.nl; ++l) {
-                const int nbias = (l == a.nl - 1) ? 32 : a.Mp[l];
+                const bool last = l == a.nl - 1;
+                const int nbias = last ? 32 : a.Mp[l];
                 if (be >= a.boff[l] && be < a.boff[l] + nbias) {
-                    const int m = be - a.boff[l];
+                    const int mm = be - a.boff[l];
+                    const int m = last ? mm : s3_mrow(mm >> 4, mm & 15);
                     if (m < a.dims[l + 1]) v = params[a.b_off[l] + m];
                 }
             }
@@ -909,15 +1049,15 @@ __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog
         const int part = w / 8192;  // 0 hi, 1 lo
         const int idx = (w % 8192) / 512, lane = (w >> 3) & 63, j = w & 7;
         const int r16 = lane & 15, g = lane >> 4;
-        int layer = -1, kind = -1, rt = 0, ks = 0;  // kind 0 fwd, 1 last fwd, 2 last dgrad, 3 hidden dgrad, 4 adjoint
+        int layer = -1, kind = -1, rt = 0, ps = 0;  // kind 0 fwd, 1 last fwd, 2 last dgrad, 3 hidden dgrad, 4 adjoint
         {
             int s = st;
             if (s < a.ns0) {
                 layer = 0;
                 kind = 0;
-                rt = s * a.r0 + idx / a.nk0;
-                ks = idx % a.nk0;
-                if (idx >= a.r0 * a.nk0 || rt >= a.nrt[0]) kind = -1;
+                rt = s * a.r0 + idx / np0;
+                ps = idx % np0;
+                if (idx >= a.r0 * np0 || rt >= a.nrt[0]) kind = -1;
             } else {
                 s -= a.ns0;
                 for (int l = 1; l < a.nl - 1 && layer < 0; ++l) {
@@ -925,7 +1065,7 @@ __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog
                         layer = l;
                         kind = 0;
                         rt = 2 * s + idx / 8;
-                        ks = idx % 8;
+                        ps = idx % 8;
                     } else {
                         s -= a.nrt[l] / 2;
                     }
@@ -935,13 +1075,13 @@ __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog
                         layer = a.nl - 1;
                         kind = 1;
                         rt = idx / 8;
-                        ks = idx % 8;
+                        ps = idx % 8;
                         if (rt > 0) kind = -1;
                     } else if (s == 1) {
                         layer = a.nl - 1;
                         kind = 2;
                         rt = idx;
-                        ks = 0;
+                        ps = 0;
                         if (rt >= a.nrtb[layer]) kind = -1;
                     } else {
                         s -= 2;
@@ -950,7 +1090,7 @@ __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog
                                 layer = l;
                                 kind = 3;
                                 rt = 2 * s + idx / 8;
-                                ks = idx % 8;
+                                ps = idx % 8;
                             } else {
                                 s -= a.nrtb[l] / 2;
                             }
@@ -959,7 +1099,7 @@ __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog
                             layer = 0;
                             kind = 4;
                             rt = 2 * s + idx / 8;
-                            ks = idx % 8;
+                            ps = idx % 8;
                             if (rt >= a.nta) kind = -1;
                         }
                     }
@@ -970,29 +1110,31 @@ __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog
         bool have = false;
         if (kind >= 0) {
             const int Mt = a.dims[layer + 1], Kt = a.dims[layer];
-            const float* W = params + a.w_off[layer];
+            const float* Wt = params + a.w_off[layer];
             int m = -1, k = -1;  // W[m][k]
-            const int row = 16 * rt + r16;
             if (kind == 0 && layer == 0) {
-                m = row;
-                k = s3_l0_feature(ks, g, j, a.L, nb);
-            } else if (kind == 0 || kind == 1) {
-                m = row;
-                k = s3_kperm(ks, g, j);
+                m = s3_mrow(rt, r16);
+                k = s3_l0_feature(ps, g, j, a.L, ng);
+            } else if (kind == 0) {
+                m = s3_mrow(rt, r16);
+                k = s3_kfeat(ps, g, j);
+            } else if (kind == 1) {
+                m = r16;  // the last layer's outputs (rows 0..2)
+                k = s3_kfeat(ps, g, j);
             } else if (kind == 2) {  // rows = input features of the last layer, k = [g hi (3), 0, g lo (3), 0]
                 if (g == 0 && (j & 3) < 3) {
                     m = j & 3;
-                    k = row;
+                    k = s3_mrow(rt, r16);
                 }
-            } else if (kind == 3) {  // W_l^T: row = input feature of layer l, k = its output (permuted)
-                m = s3_kperm(ks, g, j);
-                k = row;
-            } else {  // adjoint: row = layer-0 operand k index 32 ks' + 8 g' + j'
-                m = s3_kperm(ks, g, j);
-                k = s3_l0_feature(row >> 5, (row >> 3) & 3, row & 7, a.L, nb);
+            } else if (kind == 3) {  // W_l^T: row = input feature of layer l, k = its output
+                m = s3_kfeat(ps, g, j);
+                k = s3_mrow(rt, r16);
+            } else {  // adjoint: row = layer-0 input slot, k = layer-0 output
+                m = s3_kfeat(ps, g, j);
+                k = s3_adj_feature(rt, r16, a.L, ng);
             }
             if (m >= 0 && k >= 0 && m < Mt && k < Kt) {
-                val = W[(size_t)m * Kt + k];
+                val = Wt[(size_t)m * Kt + k];
                 have = true;
             }
         }
@@ -1009,22 +1151,22 @@ __global__ void k_pack3(const float* __restrict__ params, u16* __restrict__ prog
 
 using namespace marf;
 
-template <int NK0T, bool FULL, int NWT>
+template <int NP0T, bool FULL>
 static hipError_t launch_step3_t(const Step2Args& a, int grid, hipStream_t s) {
-    hipError_t e = ensure_dynamic_lds((const void*)k_step3<NK0T, FULL, NWT>, (size_t)a.lds_total);
+    hipError_t e = ensure_dynamic_lds((const void*)k_step3<NP0T, FULL>, (size_t)a.lds_total);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_step3<NK0T, FULL, NWT>), dim3(grid), dim3(NWT * 64), (size_t)a.lds_total, s, a);
+    hipLaunchKernelGGL((k_step3<NP0T, FULL>), dim3(grid), dim3(s3::NW * 64), (size_t)a.lds_total, s, a);
     return hipGetLastError();
 }
 
-// full = every hidden layer 256 wide (the host checks): L <= 8 and L <= 16 get their own code; the
-// generic instantiation covers the rest.  8 waves per block (two per SIMD).
+// full = every hidden layer 256 wide (the host checks): 2 and 3 layer-0 pairs (L <= 12, L <= 20)
+// get their own code; the generic instantiation covers the rest.  8 waves per block.
 bool marf_step3_nw_ok(bool, int, int nw) { return nw == 8; }
 hipError_t marf_launch_step3(const Step2Args& a, bool full, int nw, int grid, hipStream_t s) {
-    if (nw != 8) return hipErrorInvalidValue;
-    if (full && a.nk0 == 2) return launch_step3_t<2, true, 8>(a, grid, s);
-    if (full && a.nk0 == 3) return launch_step3_t<3, true, 8>(a, grid, s);
-    return launch_step3_t<s3::NK0MAX, false, 8>(a, grid, s);
+    if (nw != 8 || a.nk0 < 1 || a.nk0 > s3::NP0MAX) return hipErrorInvalidValue;
+    if (full && a.nk0 == 2) return launch_step3_t<2, true>(a, grid, s);
+    if (full && a.nk0 == 3) return launch_step3_t<3, true>(a, grid, s);
+    return launch_step3_t<s3::NP0MAX, false>(a, grid, s);
 }
 
 hipError_t marf_launch_pack3(const float* params, void* prog, float* bias_out, int* kmap, const Pack2Args& a,

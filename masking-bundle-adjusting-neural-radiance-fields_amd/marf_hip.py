@@ -63,6 +63,15 @@ _SIGS = {
                                    _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_step_backward": (_c_int, [_c_vp, ctypes.POINTER(Geometry), _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                                     _c_vp]),
+    "marf_step_backward_ev": (_c_int, [_c_vp, ctypes.POINTER(Geometry), _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
+                                       _c_vp, ctypes.POINTER(_c_vp), _c_vp]),
+    "marf_net_layer_count": (_c_int, [_c_vp]),
+    "marf_net_layer_span": (_c_int, [_c_vp, _c_int, ctypes.POINTER(_c_ll), ctypes.POINTER(_c_ll)]),
+    "marf_comm_unique_id": (_c_int, [_c_vp, _c_sz]),
+    "marf_comm_create": (_c_int, [_c_vp, _c_int, _c_int, _c_int, ctypes.POINTER(_c_vp)]),
+    "marf_comm_destroy": (None, [_c_vp]),
+    "marf_allreduce_grads": (_c_int, [_c_vp, _c_vp, _c_sz, _c_vp]),
+    "marf_allreduce_grads_layers": (_c_int, [_c_vp, _c_vp, _c_vp, ctypes.POINTER(_c_vp), _c_vp]),
     "marf_mse_workspace_bytes": (_c_sz, []),
     "marf_edge_map": (_c_int, [_c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp]),
     "marf_erode_rect": (_c_int, [_c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_vp, _c_vp]),
@@ -369,6 +378,11 @@ class Net:
         self.param_count = lib().marf_net_param_count(h)
         self.packed_bytes = lib().marf_net_packed_bytes(h)
         self.step_kernel = lib().marf_net_step_kernel(h).decode()
+        self.layer_spans = []  # (offset, length) of W_l then b_l in the flat parameter vector
+        for l in range(lib().marf_net_layer_count(h)):
+            off, n = ctypes.c_longlong(), ctypes.c_longlong()
+            _check(lib().marf_net_layer_span(h, l, ctypes.byref(off), ctypes.byref(n)))
+            self.layer_spans.append((off.value, n.value))
 
     @property
     def handle(self):
@@ -616,9 +630,12 @@ class _PlanarStepFunction(torch.autograd.Function):
         dh_local = alloc(Bl, 8, device=w.device, dtype=torch.float32)
         if d_loss is not None:
             gout = _f32(d_loss.reshape(1).to(torch.float32), "grad")
-            _check(lib().marf_step_backward(engine.net.handle, ctypes.byref(geo), _ptr(ctx.saved_buf), _ptr(ctx.h_local),
-                                            engine.lie_batch(w.shape[0]), _ptr(gout), _ptr(stats), _ptr(dflat),
-                                            _ptr(dh_local), _stream(w)))
+            ev = engine.grad_events  # per-layer "gradient final" events for a bucketed all-reduce (or None)
+            _check(lib().marf_step_backward_ev(engine.net.handle, ctypes.byref(geo), _ptr(ctx.saved_buf),
+                                               _ptr(ctx.h_local), engine.lie_batch(w.shape[0]), _ptr(gout), _ptr(stats),
+                                               _ptr(dflat), _ptr(dh_local), ev.array if ev is not None else None,
+                                               _stream(w)))
+            engine.events_for = dflat.data_ptr() if ev is not None and d_rgb is None else None
         if d_rgb is not None:
             # gradient reaching the prediction directly: general path (forward with saving + backward)
             with torch.enable_grad():
@@ -664,6 +681,8 @@ class Engine:
         self._packed_version = None
         self.last_flat_grad = None
         self.last_stats = None
+        self.grad_events = None  # GradEvents: set by the Model for the bucketed gradient all-reduce
+        self.events_for = None   # data_ptr of the flat gradient those events last marked
 
     def lie_batch(self, B):
         return self._lie_batch if self._lie_batch > 0 else B
@@ -687,6 +706,55 @@ class Engine:
         self.net.pack(flat, self._packed)
         self._packed_version = ver
         return self._packed
+
+
+class GradEvents:
+    """One torch event per MLP layer, handed to marf_step_backward_ev: event l is recorded on the
+    step's stream when layer l's gradient is final (last layer first), so each layer's all-reduce can
+    start while the weight gradients of the others still run."""
+
+    def __init__(self, n_layers, device):
+        self.events = []
+        for _ in range(n_layers):
+            e = torch.cuda.Event()
+            e.record(torch.cuda.current_stream(device))  # (torch creates the HIP event at first record)
+            self.events.append(e)
+        self.array = (_c_vp * n_layers)(*[e.cuda_event for e in self.events])
+
+
+class Comm:
+    """RCCL communicator of the C ABI (marf_comm_*), for hosts without torch.distributed: rank 0's
+    unique_id() bytes go to every rank, each then joins with Comm(uid, world, rank, device)."""
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(128)
+        _check(lib().marf_comm_unique_id(buf, 128))
+        return buf.raw
+
+    def __init__(self, uid, world, rank, device):
+        h = _c_vp()
+        _check(lib().marf_comm_create(ctypes.c_char_p(bytes(uid)), world, rank, device, ctypes.byref(h)))
+        self.handle = h
+
+    def allreduce(self, flat):
+        """In-place fp32 sum over ranks on the tensor's current stream."""
+        _check(lib().marf_allreduce_grads(self.handle, _ptr(_f32(flat, "gradient")), flat.numel(), _stream(flat)))
+
+    def allreduce_layers(self, net, flat, events):
+        """Per-layer sums, each after its layer's event, on the communicator's stream; the current
+        stream waits for the last."""
+        _check(lib().marf_allreduce_grads_layers(self.handle, net.handle, _ptr(_f32(flat, "gradient")), events.array,
+                                                 _stream(flat)))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                lib().marf_comm_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self.handle = None
 
 
 def flat_view(tensors):

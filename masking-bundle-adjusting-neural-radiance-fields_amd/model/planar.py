@@ -100,6 +100,8 @@ class Model(torch.nn.Module):
         self.graph = Graph(self.opt).to(self.opt.device)
         if self.world > 1:
             self.graph.set_shard(self.rank, self.world, self.images)
+            if self.opt.device != "cpu":
+                self._grad_engine()  # arm the per-layer gradient events before the first backward
 
     def setup_optimizer(self):
         log.info("setting up optimizers...")
@@ -173,12 +175,53 @@ class Model(torch.nn.Module):
         loss.update(all=loss_all)
         return loss
 
+    def _grad_engine(self):
+        """The neural image's engine, with per-layer gradient events armed for a bucketed exchange
+        (MARF_GRAD_BUCKETS=0: the flat all-reduce after the whole backward)."""
+        eng = self.graph.neural_image.engine(torch.device(self.opt.device))
+        if eng.grad_events is None and os.environ.get("MARF_GRAD_BUCKETS", "1") != "0":
+            eng.grad_events = marf_hip.GradEvents(len(eng.net.layer_spans), torch.device(self.opt.device))
+        return eng
+
     def all_reduce_grads(self):
-        """Sum the shared MLP gradient over ranks (RCCL over xGMI); warp rows are rank-local."""
+        """Sum the shared MLP gradient over ranks (RCCL over xGMI); warp rows are rank-local.
+
+        Bucketed per layer: the fused step's backward marks each layer's gradient
+        final as it finishes (last layer first, marf_step_backward_ev), and that layer's all-reduce
+        starts on a side stream right then, overlapping the weight gradients still running; the
+        step's stream waits for the last bucket before the optimizer reads the sums.  The flat path
+        (one all-reduce of the whole vector) covers the unfused step and MARF_GRAD_BUCKETS=0.
+        MARF_GRAD_COMM=marf exchanges through the C ABI's own RCCL communicator (marf_comm_*) instead
+        of torch.distributed's."""
         if self.world <= 1:
             return
         grads = [p.grad for p in self.graph.neural_image.mlp.parameters()]
         flat = marf_hip.flat_view(grads)
+        eng = self._grad_engine()
+        bucketed = flat is not None and eng.grad_events is not None and eng.events_for == flat.data_ptr()
+        if flat is not None and os.environ.get("MARF_GRAD_COMM") == "marf":
+            if getattr(self, "_marf_comm", None) is None:
+                uid = [marf_hip.Comm.unique_id() if self.rank == 0 else None]
+                torch.distributed.broadcast_object_list(uid, src=0)
+                self._marf_comm = marf_hip.Comm(uid[0], self.world, self.rank, flat.device.index)
+            if bucketed:
+                self._marf_comm.allreduce_layers(eng.net, flat, eng.grad_events)
+            else:
+                self._marf_comm.allreduce(flat)
+            return
+        if bucketed:
+            if getattr(self, "_comm_stream", None) is None:
+                self._comm_stream = torch.cuda.Stream(flat.device)
+            side, works = self._comm_stream, []
+            for l in reversed(range(len(eng.net.layer_spans))):
+                off, n = eng.net.layer_spans[l]
+                side.wait_event(eng.grad_events.events[l])
+                with torch.cuda.stream(side):
+                    works.append(torch.distributed.all_reduce(flat[off:off + n], async_op=True))
+            for w in works:
+                w.wait()
+            torch.cuda.current_stream(flat.device).wait_stream(side)
+            return
         if flat is not None:
             torch.distributed.all_reduce(flat)
         else:

@@ -72,7 +72,8 @@ def _run(rank, world, port, precision, out, config="c1"):
             def __len__(self):
                 return 1
         var = edict(idx=torch.arange(opt.batch_size), images=m.images)
-        losses, grads = [], None
+        init = [p.detach().cpu().numpy().copy() for p in m.graph.neural_image.mlp.parameters()]
+        losses, grads, dh = [], None, None
         for s in range(STEPS):
             loss = m.train_iteration(var, _Loader())
             if m.rank == 0:
@@ -83,14 +84,47 @@ def _run(rank, world, port, precision, out, config="c1"):
             losses.append(float(lv))
             if s == 0:
                 grads = [p.grad.detach().cpu().numpy().copy() for p in m.graph.neural_image.mlp.parameters()]
+                dh = m.graph.warp_param.weight.grad.detach().cpu().numpy().copy()
         warps = m.gathered_warps().detach().cpu().numpy()
         params = [p.detach().cpu().numpy().copy() for p in m.graph.neural_image.mlp.parameters()]
         if rank == 0:
             np.savez(out, losses=np.array(losses), warps=warps, shard=np.array(m.graph.shard or (0, opt.batch_size)),
-                     **{f"g{i}": a for i, a in enumerate(grads)}, **{f"p{i}": a for i, a in enumerate(params)})
+                     dh=dh, **{f"g{i}": a for i, a in enumerate(grads)}, **{f"p{i}": a for i, a in enumerate(params)},
+                     **{f"i{i}": a for i, a in enumerate(init)})
     finally:
         if world > 1:
             dist.destroy_process_group()
+
+
+def _spawn(world, precision, out, config, env=None):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    saved = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})  # (spawned children copy the environment at start)
+    try:
+        procs = [ctx.Process(target=_run, args=(r, world, port, precision, out, config)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+            assert p.exitcode == 0
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return np.load(out)
+
+
+def test_bucketed_allreduce_equals_flat(tmp_path):
+    """The per-layer (bucketed, overlapped) gradient all-reduce and the flat one give the same bits:
+    2 ranks on the C1 batch, bf16x3, 3 full iterations."""
+    a = _spawn(2, "bf16x3", str(tmp_path / "bucketed.npz"), "c1")
+    b = _spawn(2, "bf16x3", str(tmp_path / "flat.npz"), "c1", env={"MARF_GRAD_BUCKETS": "0"})
+    for k in a.files:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
 @pytest.mark.parametrize("precision,world,config", [("fp32", 2, "c1"), ("bf16x3", 2, "c1"), ("bf16x3", 4, "c1"),
@@ -98,23 +132,10 @@ def _run(rank, world, port, precision, out, config="c1"):
 def test_sharded_step_matches_single(precision, world, config, tmp_path):
     """world 2 / 4 on the C1 batch; world 8 on BASELINE config 4's partition (512 patches, 64 per
     rank, reduced crop): first-step MLP gradients, losses, and warps / parameters after 3 steps equal
-    the single-process run within 1e-5."""
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    port = _free_port()
-    out2 = str(tmp_path / "sharded.npz")
-    procs = [ctx.Process(target=_run, args=(r, world, port, precision, out2, config)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(timeout=300)
-        assert p.exitcode == 0
-    out1 = str(tmp_path / "one.npz")
-    p1 = ctx.Process(target=_run, args=(0, 1, port, precision, out1, config))
-    p1.start()
-    p1.join(timeout=300)
-    assert p1.exitcode == 0
-    a, b = np.load(out1), np.load(out2)
+    the single-process run within 1e-5 (C4: see below); on C4 the first step is also checked against
+    the oracle (oracle.PlanarStep)."""
+    b = _spawn(world, precision, str(tmp_path / "sharded.npz"), config)
+    a = _spawn(1, precision, str(tmp_path / "one.npz"), config)
     nb = C4_PATCHES if config == "c4" else 5
     assert tuple(b["shard"]) == (0, nb // world)
     np.testing.assert_allclose(b["losses"], a["losses"], rtol=1e-5)
@@ -123,16 +144,77 @@ def test_sharded_step_matches_single(precision, world, config, tmp_path):
         ga, gb = a[f"g{i}"], b[f"g{i}"]
         assert np.abs(gb - ga).max() <= 1e-5 * np.abs(ga).max() + 1e-12, (i, np.abs(gb - ga).max(), np.abs(ga).max())
     # warps / parameters after 3 steps: 1e-5 on the C1 batch.  On the 512-patch C4 partition Adam
-    # amplifies the ~1e-7 summation-order difference of MLP-gradient entries near zero (its first
-    # update is lr g / (|g| + eps)): measured on fp32 and bf16x3, 17 of 4096 warp entries of the
-    # 16x16 patches move by up to 3.5e-5 after 3 steps and 1-3 of 65,536 weights of a layer by up
-    # to 2.8e-4.  There: at most 1 in 100 entries beyond 1e-5, none beyond lr (one Adam step).
+    # amplifies the ~1e-7 summation-order difference of MLP-gradient entries near zero: its first
+    # update is lr g / (|g| + eps) ~ lr sign(g) for every |g| >> eps, so an entry whose first-step
+    # gradient is of the order of that rounding difference (|g| <= 1e-4 of its tensor's max) can move
+    # by up to 2 lr between the two runs.  Measured (round 3): 17 of 4096 warp entries up to 3.5e-5,
+    # 1-3 of 65,536 weights of a layer up to 2.8e-4, all of them such near-zero-gradient entries.
+    # Held here: warps <= 1e-4 everywhere; parameters <= 1e-4 wherever the first-step gradient is
+    # above 1e-4 of its max, and at most 8 near-zero entries per tensor beyond 1e-4.
     if config == "c4":
-        pairs = [(b["warps"], a["warps"])] + [(b[f"p{i}"], a[f"p{i}"]) for i in range(n)]
-        for x, y in pairs:
-            d = np.abs(x - y)
-            assert (d > 1e-5).mean() <= 1e-2 and d.max() <= 1e-3, ((d > 1e-5).sum(), d.max())
+        d = np.abs(b["warps"] - a["warps"])
+        print("C4 warps after 3 steps: max", d.max(), "beyond 1e-5:", int((d > 1e-5).sum()))
+        assert d.max() <= 1e-4, d.max()
+        for i in range(n):
+            d = np.abs(b[f"p{i}"] - a[f"p{i}"])
+            big = np.abs(a[f"g{i}"]) > 1e-4 * np.abs(a[f"g{i}"]).max()
+            print(f"C4 param {i}: max {d.max():.3g} (gradient above 1e-4 of max: {d[big].max() if big.any() else 0:.3g}), "
+                  f"beyond 1e-4: {int((d > 1e-4).sum())}")
+            assert (d[big].max() if big.any() else 0) <= 1e-4 and int((d > 1e-4).sum()) <= 8
+        _c4_first_step_vs_oracle(a, precision, n)
     else:
         np.testing.assert_allclose(b["warps"], a["warps"], atol=1e-5, rtol=0)
         for i in range(n):
             np.testing.assert_allclose(b[f"p{i}"], a[f"p{i}"], atol=1e-5, rtol=0)
+
+
+def _c4_first_step_vs_oracle(a, precision, n):
+    """The single-process first step of the C4 partition against oracle.PlanarStep (numpy + C, fp32):
+    MLP gradients and the warp gradient within 2e-4 of their max and cosine >= 0.99999 (fp32; a
+    131,072-pixel sum in another fp32 order), within the north_star bf16 1e-2 and cosine >= 0.9999
+    for bf16x3."""
+    import oracle
+    g = np.random.default_rng(0)  # _run's synthetic C4 targets
+    rgb = g.random((C4_PATCHES, 3, C4_CROP, C4_CROP)).astype(np.float32)
+    mask = (g.random((C4_PATCHES, 1, C4_CROP, C4_CROP)) < 0.85).astype(np.float32)
+    params = [(a[f"i{2 * k}"], a[f"i{2 * k + 1}"]) for k in range(n // 2)]
+    cfg = dict(H=2 * C4_CROP, W=2 * C4_CROP, patch_H=C4_CROP, patch_W=C4_CROP, L=16, c2f=[0, 0.4], max_iter=3000,
+               lr=1e-3, lr_warp=1e-3, fix_first=True, use_edges=False, alpha_initial=0.0, alpha_final=1.0)
+    r = oracle.PlanarStep(cfg, params, np.zeros((C4_PATCHES, 8), np.float32), rgb, mask).step()
+    tol, cmin = (2e-4, 0.99999) if precision == "fp32" else (1e-2, 0.9999)
+    pairs = [(a[f"g{2 * k}"], r["grads"][k][0]) for k in range(n // 2)] + \
+            [(a[f"g{2 * k + 1}"], r["grads"][k][1]) for k in range(n // 2)] + [(a["dh"], r["dh"])]
+    for got, ref in pairs:
+        err = np.abs(got - ref).max() / (np.abs(ref).max() + 1e-30)
+        cos = float(got.ravel().astype(np.float64) @ ref.ravel() / (np.linalg.norm(got) * np.linalg.norm(ref) + 1e-30))
+        print(f"C4 first step vs oracle ({precision}): err {err:.3g} cos {cos:.7f}")
+        assert err <= tol and cos >= cmin, (err, cos)
+
+
+def test_marf_comm_rccl_one_rank():
+    """The C ABI's own RCCL communicator (marf_comm_*, for hosts without torch.distributed) on one
+    rank: the flat and the per-layer all-reduce run through librccl.so and leave the gradient as it
+    was (a sum over one rank); the per-layer one waits on the layer events and joins the caller's
+    stream."""
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    import marf_hip
+    dev = torch.device("cuda:0")
+    uid = marf_hip.Comm.unique_id()
+    assert len(uid) == 128
+    comm = marf_hip.Comm(uid, 1, 0, 0)
+    x = torch.randn(100003, device=dev)
+    y = x.clone()
+    comm.allreduce(y)
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)
+    net = marf_hip.Net([66, 256, 256, 256, 256, 3], 16, marf_hip.MARF_BF16X3)
+    assert [n for _, n in net.layer_spans] == [256 * 66 + 256] + [256 * 256 + 256] * 3 + [3 * 256 + 3]
+    flat = torch.randn(net.param_count, device=dev)
+    ref = flat.clone()
+    ev = marf_hip.GradEvents(len(net.layer_spans), dev)
+    comm.allreduce_layers(net, flat, ev)
+    torch.cuda.synchronize()
+    assert torch.equal(flat, ref)
+    del comm

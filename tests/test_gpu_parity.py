@@ -1013,6 +1013,89 @@ def test_c3_two_patch_step_vs_oracle(precision, tmp_path, monkeypatch):
         assert o["grad_err"] <= 2 * o["grad_err_ref32"] and o["dh_err"] <= 2 * o["dh_err_ref32"], o
 
 
+_STEP3_CASES = {
+    # name: (B, crop, L, hidden); tile counts per block of the 256-block grid in brackets
+    "c1": None,                                   # cat_batch3, 5 x 180x240, L=8 (6 or 7)
+    "c3x2": (2, 256, 16, [256] * 4),              # C3 shape (4), odd layer-0 chunk count (5)
+    "c3x3-L10": (3, 256, 10, [256] * 4),          # even layer-0 chunk count (4) (6)
+    "L16-1tile": (2, 100, 16, [256] * 4),         # 158 tiles: one tile per block, 98 idle blocks
+    "narrow": (2, 64, 8, [128, 96, 128]),         # the generic instantiation (widths < 256)
+}
+
+
+def _kernel_model(case, kernel, tmp_path, monkeypatch):
+    """The bf16x3 product model of a _STEP3_CASES case whose step runs `kernel` (MARF_STEP3 is read
+    when the engine's net is created)."""
+    import time
+    from util import EasyDict as edict
+    if kernel == "k_step3":
+        monkeypatch.setenv("MARF_STEP3", "1")
+    else:
+        monkeypatch.delenv("MARF_STEP3", raising=False)
+    inputs = None
+    if _STEP3_CASES[case] is None:
+        m, var = c1_setup("bf16x3", tmp_path / kernel)
+    else:
+        B, crop, L, hidden = _STEP3_CASES[case]
+        m, var, inputs = _synthetic_setup("bf16x3", tmp_path / kernel, B, crop, L, hidden)
+        m.timer = edict(start=time.time(), it_mean=None)
+    assert m.graph.neural_image.engine(torch.device(DEV)).net.step_kernel == kernel
+    monkeypatch.delenv("MARF_STEP3", raising=False)
+    return m, var, inputs
+
+
+@pytest.mark.parametrize("kernel", ["k_step2", "k_step3"])
+def test_bf16x3_odd_width_vs_oracle(kernel, tmp_path, monkeypatch):
+    """Hidden widths of 32 mod 64 (an odd number of 32-row tiles; here 96) on the split-bf16 step
+    kernels, against the oracle (rgb, loss) and the reference ops in float64 (gradients): the bf16x3
+    forward bound (rgb <= 1e-5) and the north_star bf16 bound on the gradients (<= 1e-2 of their max),
+    with cosine >= 0.9999.  (k_step2 lost the ReLU mask word of such a layer's last row tile before
+    round 4.)"""
+    m, var, inputs = _kernel_model("narrow", kernel, tmp_path, monkeypatch)
+    o = _compare_step(m, var, inputs, "bf16x3", len(_STEP3_CASES["narrow"][3]) + 1)
+    assert o["rgb"] <= 1e-5 and o["loss"] <= 1e-5, o
+    assert o["grad_err"] <= 1e-2 and o["dh_err"] <= 1e-2, o
+    assert o["grad_cos"] >= 0.9999 and o["dh_cos"] >= 0.9999, o
+
+
+@pytest.mark.parametrize("case", list(_STEP3_CASES))
+def test_step3_bitwise_equals_step2(case, tmp_path, monkeypatch):
+    """k_step3 (two waves per SIMD) computes k_step2's arithmetic: the first step's rgb, loss, every
+    MLP gradient and the warp gradient are bit-identical, and so are the parameters and warps after
+    two more full training iterations (Adam, progress, fix_first).  This is what lets the faster
+    kernel inherit k_step2's seed-3 run (test_c1_3000_iterations_psnr_and_warps)."""
+    res = {}
+    for kernel in ("k_step2", "k_step3"):
+        m, var, _ = _kernel_model(case, kernel, tmp_path, monkeypatch)
+        v, loss = one_step_grads(m, var)
+        r = {"rgb": v.rgb_prediction.detach().cpu(), "loss": loss.rgb.detach().cpu(),
+             "dh": m.graph.warp_param.weight.grad.detach().cpu()}
+        for i, lay in enumerate(m.graph.neural_image.mlp):
+            r[f"dW{i}"] = lay.weight.grad.detach().cpu()
+            r[f"db{i}"] = lay.bias.grad.detach().cpu()
+        m.optim.step()
+        m.graph.warp_param.weight.data[0] = 0
+        for _ in range(2):
+            r.setdefault("losses", []).append(float(m.train_iteration(var, _Loader()).rgb))
+            m.graph.warp_param.weight.data[0] = 0
+        r["warp"] = m.graph.warp_param.weight.detach().cpu()
+        for i, lay in enumerate(m.graph.neural_image.mlp):
+            r[f"W{i}"] = lay.weight.detach().cpu()
+        res[kernel] = r
+    a, b = res["k_step2"], res["k_step3"]
+    bad = []
+    for k in a:
+        if k == "losses":
+            if a[k] != b[k]:
+                bad.append((k, a[k], b[k]))
+        elif not torch.equal(a[k], b[k]):
+            d = (a[k].double() - b[k].double()).abs()
+            bad.append((k, int((d > 0).sum()), float(d.max())))
+    for x in bad:
+        print("differs:", x)
+    assert not bad, [x[0] for x in bad]
+
+
 @pytest.mark.parametrize("c2f", [(0, 0.4), None], ids=["c2f", "noc2f"])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_c5_shape_step_vs_oracle(precision, c2f, tmp_path):

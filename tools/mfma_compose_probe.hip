@@ -48,6 +48,22 @@ __global__ void run16(const u16* A, const u16* B, int n, const float* init, floa
     for (int r = 0; r < 4; ++r) out[l * 4 + r] = acc[r];
 }
 
+// as run16, with a per-MFMA B lane-group pattern (blgp 0: as is, 1: lanes 0-31 also into 32-63,
+// 2: lanes 32-63 also into 0-31)
+__global__ void run16g(const u16* A, const u16* B, const int* g, int n, const float* init, float* out) {
+    const int l = threadIdx.x;
+    f32x4 acc;
+    for (int r = 0; r < 4; ++r) acc[r] = init[l * 4 + r];
+    for (int i = 0; i < n; ++i) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + ((size_t)i * 64 + l) * 8);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(B + ((size_t)i * 64 + l) * 8);
+        if (g[i] == 1) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 1);
+        else if (g[i] == 2) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 2);
+        else acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+    }
+    for (int r = 0; r < 4; ++r) out[l * 4 + r] = acc[r];
+}
+
 static u16 tobf(float f) {
     unsigned u;
     std::memcpy(&u, &f, 4);
@@ -119,17 +135,31 @@ struct Runner {
                 if (row < 16 && col < 16) out[row][col] = O[l * 16 + r];
             }
     }
-    void go16(const std::vector<std::pair<const Blk*, const Blk*>>& seq, const float init[16][16], float out[16][16]) {
+    // blgp: per MFMA; the B fragments of seq are built as given, the pattern applied by the hardware
+    void go16(const std::vector<std::pair<const Blk*, const Blk*>>& seq, const float init[16][16], float out[16][16],
+              const std::vector<std::pair<const Blk*, const Blk*>>* bseq = nullptr, const std::vector<int>* blgp = nullptr) {
         const int n = (int)seq.size();
-        std::vector<u16> A(n * 512), B(n * 512);
-        for (int i = 0; i < n; ++i) frag16(seq[i].first, seq[i].second, &A[i * 512], &B[i * 512]);
+        std::vector<u16> A(n * 512), B(n * 512), tmp(512);
+        for (int i = 0; i < n; ++i) {
+            frag16(seq[i].first, seq[i].second, &A[i * 512], &B[i * 512]);
+            if (bseq) frag16((*bseq)[i].first, (*bseq)[i].second, tmp.data(), &B[i * 512]);
+        }
         std::vector<float> I(64 * 4), O(64 * 4);
         for (int l = 0; l < 64; ++l)
             for (int r = 0; r < 4; ++r) I[l * 4 + r] = init[4 * (l >> 4) + r][l & 15];
         hipMemcpy(dA, A.data(), A.size() * 2, hipMemcpyHostToDevice);
         hipMemcpy(dB, B.data(), B.size() * 2, hipMemcpyHostToDevice);
         hipMemcpy(dI, I.data(), I.size() * 4, hipMemcpyHostToDevice);
-        run16<<<1, 64>>>(dA, dB, n, dI, dO);
+        if (blgp) {
+            int* dg;
+            hipMalloc(&dg, n * 4);
+            hipMemcpy(dg, blgp->data(), n * 4, hipMemcpyHostToDevice);
+            run16g<<<1, 64>>>(dA, dB, dg, n, dI, dO);
+            hipDeviceSynchronize();
+            hipFree(dg);
+        } else {
+            run16<<<1, 64>>>(dA, dB, n, dI, dO);
+        }
         hipMemcpy(O.data(), dO, O.size() * 4, hipMemcpyDeviceToHost);
         for (int l = 0; l < 64; ++l)
             for (int r = 0; r < 4; ++r) out[4 * (l >> 4) + r][l & 15] = O[l * 4 + r];
@@ -148,7 +178,7 @@ int main() {
     std::uniform_real_distribution<float> U(-1.f, 1.f);
     Runner R;
     const int NCH = 16;  // 16-k chunks: K = 256
-    long long tot[4] = {0, 0, 0, 0}, outs[4] = {0, 0, 0, 0};
+    long long tot[5] = {0, 0, 0, 0, 0}, outs[5] = {0, 0, 0, 0, 0};
     for (int trial = 0; trial < 48; ++trial) {
         const float ws = std::ldexp(1.f, (int)(rng() % 9) - 6), xs = std::ldexp(1.f, (int)(rng() % 9) - 4);
         // weights W [16][256] (hi + lo), activations X [256][16] (hi + lo, ReLU'd, ~40% zeros), dz [256][16]
@@ -235,6 +265,30 @@ int main() {
             tot[2] += ndiff(r2, r3);
             outs[2] += 256;
         }
+        // (4) dgrad from ONE register D = [dz(2s) | dz(2s+1)] with the B lane-group pattern:
+        //     [hd(2s) | ld(2s)] with blgp 1 (lanes 0-31 into 32-63), [hd(2s+1) | ld(2s+1)] with blgp 2
+        {
+            float z[16][16] = {};
+            std::vector<Blk> s2;
+            for (int c = 0; c < NCH; ++c) {
+                s2.push_back(hd[c]);
+                s2.push_back(ld[c]);
+            }
+            R.go32(s2, z, r2);
+            std::vector<std::pair<const Blk*, const Blk*>> s3, b3;
+            std::vector<int> g;
+            for (int s = 0; s < NCH / 2; ++s) {
+                s3.push_back({&hd[2 * s], &ld[2 * s]});
+                b3.push_back({&hd[2 * s], &hd[2 * s + 1]});  // the B fragment as the register holds it
+                g.push_back(1);
+                s3.push_back({&hd[2 * s + 1], &ld[2 * s + 1]});
+                b3.push_back({&hd[2 * s], &hd[2 * s + 1]});
+                g.push_back(2);
+            }
+            R.go16(s3, z, r3, &b3, &g);
+            tot[4] += ndiff(r2, r3);
+            outs[4] += 256;
+        }
         // (3) dW_last: one K = 32 16x16x32 MFMA from zero vs two chained halves
         {
             float z[16][16] = {};
@@ -250,8 +304,9 @@ int main() {
             outs[3] += 256;
         }
     }
-    const char* names[4] = {"forward 3-term composition (16 chunks)", "forward, 5 chunks (odd tail)",
-                            "dgrad [hd|ld] composition", "K=32 split into two chained halves"};
-    for (int i = 0; i < 4; ++i) printf("%-42s: %lld of %lld outputs differ\n", names[i], tot[i], outs[i]);
+    const char* names[5] = {"forward 3-term composition (16 chunks)", "forward, 5 chunks (odd tail)",
+                            "dgrad [hd|ld] composition", "K=32 split into two chained halves",
+                            "dgrad from one register, blgp 1 / 2"};
+    for (int i = 0; i < 5; ++i) printf("%-42s: %lld of %lld outputs differ\n", names[i], tot[i], outs[i]);
     return 0;
 }
