@@ -68,14 +68,22 @@ def step_kernel_bytes(S, Kp0, hidden, elem):
     }
 
 
-def pmc_traffic(cfg, precision, kernel):
+def pmc_traffic(cfg, precision, kernel, symbol_prefix):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/pmc_traffic.json, written by tools/pmc_summary.py --traffic)."""
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py --traffic), or None unless the entry
+    was measured on the library loaded now (same marf_source_hash) and on the same kernel
+    instantiation kind (its symbol starts with `symbol_prefix`, e.g. the step kernel this size
+    picked): a number from another build or kernel is never reported as this run's traffic."""
+    import marf_hip
     try:
         d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))[f"{cfg}/{precision}"]
-        e = d[kernel]
-        return e["hbm_read_bytes"] + e["hbm_write_bytes"], d["source"]
-    except (OSError, KeyError, ValueError):
+        e = d["kernels"][kernel]
+        if d["source_hash"] != marf_hip.lib().marf_source_hash().decode():
+            return None
+        if symbol_prefix and not e["symbol"].startswith(symbol_prefix):
+            return None
+        return e["hbm_read_bytes"] + e["hbm_write_bytes"], f"{d['source']}; {e['symbol']}; source hash {d['source_hash']}"
+    except (OSError, KeyError, ValueError, TypeError):
         return None
 
 
@@ -337,7 +345,7 @@ def main():
         alg, issued = kflops[dom]
         alg_bytes = 28 * px_local if dom == "mlp_step" else None
         design = step_kernel_bytes(S, Kp0, hidden, 2 if args.precision != "fp32" else 4).get(dom)
-        tr = pmc_traffic(args.config, args.precision, dom)
+        tr = pmc_traffic(args.config, args.precision, dom, step_kernel if dom == "mlp_step" else "k_wgrad")
         roof = {"bound": "mfma", "achieved": alg / avg_s / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
                 "frac": alg / avg_s / peak, "traffic": tr[0] if tr else None,
                 "kernel": dom, "launches_per_step": prof[dom][1] / args.steps,

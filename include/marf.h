@@ -111,6 +111,9 @@ int marf_prologue_probe(const marf_geometry* geo, const marf_c2f* c2f, int L, co
  * Flat fp32 parameter vector layout = NeuralImageFunction.mlp parameters in module order:
  * W0 [dims1][dims0], b0 [dims1], W1, b1, ...  (nn.Linear layout). */
 int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** out);
+/* As marf_net_create, with the pixels one fused step will process on this GPU (0 = unknown): it picks
+ * the faster of the split recipe's two step kernels for that size (they compute the same bits). */
+int marf_net_create_hint(int n_layers, const int* dims, int L, int dtype, long long pixels_hint, marf_net** out);
 void marf_net_destroy(marf_net* net);
 long long marf_net_param_count(const marf_net* net);
 size_t marf_net_packed_bytes(const marf_net* net);

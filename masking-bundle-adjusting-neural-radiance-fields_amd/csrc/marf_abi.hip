@@ -97,6 +97,7 @@ static bool step2_env_enabled() {
 }
 
 int marf_step3_wave_lds_bytes();
+static int device_cus();
 
 // variant 3 (marf_step3.hip): k_step2's arithmetic on 16 pixels per wave (16x16x32 MFMAs, 8 waves,
 // 128-pixel block tiles as k_step2), 32 KB stages of 16-row tiles -- layer 0: r0 row tiles of nk0
@@ -147,7 +148,11 @@ static void plan_step3_net(marf_net* n) {
 
 // Which pixel-per-wave variant (marf_step2.hip) runs this net, its weight-program shape and the
 // byte layout of the program / bias table / layer-0 column map appended to the packed buffer.
-static void plan_step2_net(marf_net* n) {
+// The split recipe has two kernels of identical arithmetic (k_step3 = k_step2 bit for bit): k_step3
+// (two waves per SIMD) is the faster one below about 48 block tiles of 128 pixels per CU (C1: 6.6,
+// -10 % kernel time), k_step2 above it (C3: 128, k_step3 +4 %); pixels_hint (the step's pixels per
+// GPU, 0 = unknown) picks it, MARF_STEP3=0 / 1 at net creation forces one.
+static void plan_step2_net(marf_net* n, long long pixels_hint) {
     Step2NetPlan& q = n->s2;
     memset(&q, 0, sizeof(q));
     q.variant = -1;
@@ -160,9 +165,11 @@ static void plan_step2_net(marf_net* n) {
     if (n->dtype != MARF_BF16X3 && !step2_env_enabled()) return;
     q.HM = 256;
     q.variant = n->dtype == MARF_BF16X3 ? 1 : 0;
-    if (q.variant == 1) {  // the two-waves-per-SIMD kernel (k_step3) on request: MARF_STEP3=1 at net creation
+    if (q.variant == 1) {
         const char* e = getenv("MARF_STEP3");
-        if (e && e[0] == '1') {
+        const bool step3 = (e && e[0]) ? e[0] == '1'
+                                       : pixels_hint > 0 && pixels_hint < 48LL * 128 * device_cus();
+        if (step3) {
             plan_step3_net(n);
             return;
         }
@@ -396,6 +403,10 @@ int marf_prologue_probe(const marf_geometry* geo, const marf_c2f* c2f, int L, co
 // ------------------------------------------------------------------ network
 
 int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** out) {
+    return marf_net_create_hint(n_layers, dims, L, dtype, 0, out);
+}
+
+int marf_net_create_hint(int n_layers, const int* dims, int L, int dtype, long long pixels_hint, marf_net** out) {
     if (!out || !dims) return fail(MARF_ERR_INVALID, "net_create: NULL argument");
     *out = nullptr;
     if (n_layers < 2 || n_layers > MARF_MAX_LAYERS)
@@ -479,7 +490,7 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
     n->param_count = off;
     n->packed_bytes = boff;
     parse_diag(n);
-    plan_step2_net(n);
+    plan_step2_net(n, pixels_hint);
     {  // defaults of the pipelined weight gradients (marf_net_set_pipeline changes them)
         const char* e = getenv("MARF_PIPE");
         n->pipe_mode = e && *e ? atoi(e) : 0;  // off: measured slower

@@ -499,9 +499,6 @@ __global__ __launch_bounds__(512, 2) void k_step3(Step2Args a) {
         dh_pending = -1;
     };
 
-#ifdef S3_SETPRIO
-    if (half) __builtin_amdgcn_s_setprio(1);
-#endif
     S3T_BEGIN(15);
     for (int ti = 0; ti < my_tiles; ++ti) {
         S3T_BEGIN(3);

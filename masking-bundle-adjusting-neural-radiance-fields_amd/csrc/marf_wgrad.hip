@@ -220,9 +220,17 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
 // Issued as inline asm: hipcc tracks its own builtin LDS-DMA and waits vmcnt(0) before the next
 // ds_read of the same LDS array, which would drain the ring; the asm form is outside its
 // bookkeeping, and the kernel counts completion itself.  lds: wave-uniform LDS byte address.
+#ifndef MARF_WG_NT
+#define MARF_WG_NT 0
+#endif
+#if MARF_WG_NT
+#define MARF_WG_POL " nt"
+#else
+#define MARF_WG_POL ""
+#endif
 MARF_DEV void glds16(const char* src, unsigned lds) {
     unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" MARF_WG_POL "\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(src), "s"(lds)
                  : "memory");
@@ -251,7 +259,7 @@ MARF_DEV int foff(int r, int c) {
 template <class P, int NBUF, int SP, int KF, bool F0 = false>
 __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     static_assert(KF == 256 || KF == 96, "feat width");
-    static_assert(!F0 || (KF == 96 && SP == 32), "feat_0 recompute: the 96-wide layer-0 stage of 32 rows");
+    static_assert(!F0 || (KF == 96 && SP % 32 == 0), "feat_0 recompute: the 96-wide layer-0 stage, 32-row blocks");
     constexpr int WR = KF == 256 ? 4 : 8, WC = 8 / WR;  // wave grid over the 256 x KF output
     constexpr int RT = 256 / 32 / WR, CT = KF / 32 / WC;
     constexpr int ZB = SP * 512;                 // bytes of the dz stage (SP rows x 256 bf16)
@@ -350,7 +358,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     // columns 64..95 (the step kernel's s2_split8 hi words: v_cvt_pk_bf16_f32 of the same fp32 values).
     // Stage st's coordinates were warped before a barrier that precedes this call.
     auto compute_f0 = [&](int st, int buf_off) {
-        const int r = threadIdx.x >> 4, sub = threadIdx.x & 15;
+#pragma unroll
+      for (int rb = 0; rb < SP; rb += 32) {
+        const int r = rb + (threadIdx.x >> 4), sub = threadIdx.x & 15;
         const float u = f0_uv[((st % (NBUF + 1)) * SP + r) * 2], v = f0_uv[((st % (NBUF + 1)) * SP + r) * 2 + 1];
         char* row = smem + buf_off + r * (KF * 2);
         const int h = sub >> 3, k0 = 2 * (sub & 7);
@@ -379,6 +389,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
             const float val = (c - 16 * ng) == 8 * hc && hc < 2 ? (hc ? v : u) : 0.f;
             *reinterpret_cast<uint32_t*>(row + 2 * c) = PrecBF16::pk2(val, 0.f);
         }
+      }
     };
     auto issue = [&](int st) {
         const unsigned buf = lds0 + (st % NBUF) * STB;
@@ -656,13 +667,19 @@ static bool wgrad_dma_enabled() {
 #ifndef MARF_WG_NBUF_0
 #define MARF_WG_NBUF_0 4
 #endif
+#ifndef MARF_WG_SP0
+#define MARF_WG_SP0 64
+#endif
+#ifndef MARF_WG_SPH
+#define MARF_WG_SPH 32
+#endif
 
 template <class P, int KF, bool F0 = false>
 static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
     a.n_chunks = n_chunks;
     a.n_oblk_c = a.K / KF;
-    constexpr int SP = 32;
-    constexpr int NBUF = KF == 256 ? MARF_WG_NBUF_H : MARF_WG_NBUF_0;  // ring depth within 160 KB of LDS
+    constexpr int SP = F0 ? MARF_WG_SP0 : KF == 256 ? MARF_WG_SPH : 32;
+    constexpr int NBUF = KF == 256 ? (SP == 64 ? 2 : MARF_WG_NBUF_H) : (SP == 64 ? 3 : MARF_WG_NBUF_0);  // ring depth within 160 KB of LDS
     const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024) + (F0 ? (9 * F0_PATCHES + 32 + (NBUF + 1) * SP * 2) * 4 : 0);
     {
         hipError_t e = ensure_dynamic_lds((const void*)k_wgrad_dma<P, NBUF, SP, KF, F0>, lds);
@@ -684,7 +701,7 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
         a.s_len = rng->s_len;
         a.rng_n = n_chunks = rng->n;
         a.part0 = rng->part0;
-        chunk = 32;  // (the stage granularity the range mode splits at)
+        chunk = 64;  // (a multiple of every stage height the range mode splits at)
     }
     a.dz = dz;
     a.feat = feat;
@@ -707,7 +724,8 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
     // LDS-DMA ring: 256-wide dz with a 256-wide (hidden) or 96-wide (layer 0, L = 16) feat
     const bool dma = M % 256 == 0 && ldz % 8 == 0 && ldz >= M && S % 32 == 0 && chunk % 32 == 0 &&
                      (long long)n_chunks * (M / 256) * ((K + 255) / 256) <= 0x7fffffff && wgrad_dma_enabled();
-    const bool dma256 = dma && K % 256 == 0 && ldf % 8 == 0 && ldf >= K, dma96 = dma && K == 96 && ldf == 96;
+    const bool dma256 = dma && K % 256 == 0 && ldf % 8 == 0 && ldf >= K && S % MARF_WG_SPH == 0 && chunk % MARF_WG_SPH == 0,
+               dma96 = dma && K == 96 && ldf == 96;
     if (rng && (dtype == 0 || !(dma256 || dma96))) return hipErrorInvalidValue;  // range mode: LDS-DMA kernel only
     if (dtype == 1) {
         if (dma256) return launch_wg_dma<PrecBF16, 256>(a, n_chunks, s);
@@ -742,7 +760,7 @@ bool marf_wgrad_range_ok(int dtype, int M, int ldz, int K, int ldf) {
 // Layer-0 weight gradient with feat_0 recomputed on chip (step kernel's feat0_recompute); bf16,
 // 256-wide layer 0, the 96-wide feat_0 of L = 13..16.  False if the shape does not qualify.
 bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk, int n_chunks, long long Np_pad) {
-    return M == 256 && ldz % 8 == 0 && ldz >= M && ldf0 == 96 && S % 32 == 0 && chunk % 32 == 0 &&
+    return M == 256 && ldz % 8 == 0 && ldz >= M && ldf0 == 96 && S % MARF_WG_SP0 == 0 && chunk % MARF_WG_SP0 == 0 &&
            (long long)n_chunks <= 0x7fffffff && Np_pad < (1 << 24) && (chunk + Np_pad - 1) / Np_pad + 1 <= F0_PATCHES;
 }
 

@@ -45,6 +45,7 @@ _SIGS = {
     "marf_prologue_probe": (_c_int, [ctypes.POINTER(Geometry), ctypes.POINTER(C2f), _c_int, _c_vp, _c_vp, _c_vp, _c_int,
                                      _c_vp]),
     "marf_net_create": (_c_int, [_c_int, ctypes.POINTER(_c_int), _c_int, _c_int, ctypes.POINTER(_c_vp)]),
+    "marf_net_create_hint": (_c_int, [_c_int, ctypes.POINTER(_c_int), _c_int, _c_int, _c_ll, ctypes.POINTER(_c_vp)]),
     "marf_net_destroy": (None, [_c_vp]),
     "marf_net_param_count": (_c_ll, [_c_vp]),
     "marf_net_packed_bytes": (_c_sz, [_c_vp]),
@@ -367,13 +368,13 @@ def posenc(coord, L, progress=None, c2f=None):
 class Net:
     """An MLP shape + padding plan in the library (marf_net)."""
 
-    def __init__(self, dims, L, dtype):
+    def __init__(self, dims, L, dtype, pixels_hint=0):
         self.dims = [int(d) for d in dims]
         self.L = int(L)
         self.dtype = dtype
         arr = (_c_int * len(self.dims))(*self.dims)
         h = _c_vp()
-        _check(lib().marf_net_create(len(self.dims) - 1, arr, self.L, dtype, ctypes.byref(h)))
+        _check(lib().marf_net_create_hint(len(self.dims) - 1, arr, self.L, dtype, int(pixels_hint), ctypes.byref(h)))
         self._h = h
         self.param_count = lib().marf_net_param_count(h)
         self.packed_bytes = lib().marf_net_packed_bytes(h)
@@ -671,8 +672,8 @@ def geo_np(engine):
 class Engine:
     """Library-side state of one NeuralImageFunction: net plan, packed weights, c2f, geometry."""
 
-    def __init__(self, dims, L, dtype, c2f, H, W, patch_H, patch_W, lie_batch=0, crop=True):
-        self.net = Net(dims, L, dtype)
+    def __init__(self, dims, L, dtype, c2f, H, W, patch_H, patch_W, lie_batch=0, crop=True, pixels_hint=0):
+        self.net = Net(dims, L, dtype, pixels_hint)
         self.c2f = c2f
         self.H, self.W, self.patch_H, self.patch_W = H, W, patch_H, patch_W
         self.crop = bool(crop)

@@ -197,8 +197,8 @@ class Model(torch.nn.Module):
             return
         grads = [p.grad for p in self.graph.neural_image.mlp.parameters()]
         flat = marf_hip.flat_view(grads)
-        eng = self._grad_engine()
-        bucketed = flat is not None and eng.grad_events is not None and eng.events_for == flat.data_ptr()
+        eng = self._grad_engine() if flat is not None and flat.is_cuda else None  # (gloo on CPU: flat)
+        bucketed = eng is not None and eng.grad_events is not None and eng.events_for == flat.data_ptr()
         if flat is not None and os.environ.get("MARF_GRAD_COMM") == "marf":
             if getattr(self, "_marf_comm", None) is None:
                 uid = [marf_hip.Comm.unique_id() if self.rank == 0 else None]
@@ -507,8 +507,12 @@ class NeuralImageFunction(torch.nn.Module):
             o = self.opt
             dims = [self.input_dim] + [int(d) for d in list(o.arch.layers)[1:]]
             ph, pw = (o.patch_H, o.patch_W) if o.use_cropped_images else (o.H, o.W)
+            # the fused step's pixels on this GPU (this rank's patches), for the library's kernel choice
+            world = torch.distributed.get_world_size() if _dist() else 1
+            hint = -(-int(o.batch_size) // world) * ph * pw
             e = marf_hip.Engine(dims, self.L, _precision(o), list(o.barf_c2f) if o.barf_c2f else None,
-                                o.H, o.W, ph, pw, lie_batch=int(o.batch_size), crop=bool(o.use_cropped_images))
+                                o.H, o.W, ph, pw, lie_batch=int(o.batch_size), crop=bool(o.use_cropped_images),
+                                pixels_hint=hint)
             self._engines[key] = e
         return e
 

@@ -9,7 +9,8 @@ for round in 1 2; do
     env $envs $L timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render > gpurun_out/ab_${TAG}_${name}_$round.json 2> gpurun_out/ab_${TAG}_${name}_$round.err || { echo "$name failed"; tail -3 gpurun_out/ab_${TAG}_${name}_$round.err; exit 1; }
     python -c "
 import json; d=json.loads(open('gpurun_out/ab_${TAG}_${name}_$round.json').read().strip().splitlines()[-1])
-print('%-10s r$round %.4g px/s  %.3f ms/step  %s %.3f ms  loss %.9g' % ('$name', d['value'], d['ms_per_step'], d['config']['step_kernel'], d['roofline']['avg_launch_ms'], d['config']['loss_rgb_last']))
+kk = d.get('kernels', {}); wg = ' '.join('%s %.3f' % (k, v['avg_ms']) for k, v in sorted(kk.items()) if k.startswith('wgrad'))
+print('%-10s r$round %.4g px/s  %.3f ms/step  %s %.3f ms  [%s]  loss %.9g' % ('$name', d['value'], d['ms_per_step'], d['config']['step_kernel'], d['roofline']['avg_launch_ms'], wg, d['config']['loss_rgb_last']))
 "
   done
 done

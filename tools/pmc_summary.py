@@ -29,7 +29,7 @@ for f in sorted(glob.glob(os.path.join(root, "pass*", "*counter_collection.csv")
 
 
 def short(k):
-    return k.split("(")[0].replace("void ", "").replace("marf::", "")[:48]
+    return k.split("(")[0].replace("void ", "").replace("marf::", "")[:64]
 
 
 rows = []
@@ -59,13 +59,16 @@ for r in rows:
             print(f"    {c:28s} {r[c]:.4g}")
 
 # bench.py reads the HBM bytes per launch of its kernels from profiles/pmc_traffic.json
-# (python tools/pmc_summary.py gpurun_out/<tag> profiles/<round>_pmc.csv --traffic c3/bf16)
+# (python tools/pmc_summary.py gpurun_out/<tag> profiles/<round>_pmc.csv --traffic c3/bf16x3 <source hash>)
+# An entry names the kernel symbol it measured and the marf_source_hash of the library that ran it;
+# bench.py reports its traffic only when both match the run (otherwise traffic: null).
 if "--traffic" in sys.argv:
     import json
-    tag = sys.argv[sys.argv.index("--traffic") + 1]
+    i = sys.argv.index("--traffic")
+    tag, src_hash = sys.argv[i + 1], sys.argv[i + 2]
     tj = os.path.join(os.path.dirname(out) if out else "profiles", "pmc_traffic.json")
     data = json.load(open(tj)) if os.path.exists(tj) else {}
-    ent = {}
+    kernels = {}
     for r in rows:
         k = r["kernel"]
         name = None
@@ -74,14 +77,17 @@ if "--traffic" in sys.argv:
         elif k.startswith("k_prologue_probe"):
             name = "prologue_probe"
         elif k.startswith("k_wgrad_dma<"):
-            name = "wgrad_hidden" if k.rstrip(">").endswith("256") else "wgrad_l0"
+            name = "wgrad_l0" if ", 96" in k else "wgrad_hidden"
         elif k.startswith("k_wgrad<"):
             name = "wgrad_hidden" if ", 2, 4" in k else "wgrad_l0"
         if name and "hbm_read_bytes" in r and "hbm_write_bytes" in r:
-            ent[name] = {"hbm_read_bytes": r["hbm_read_bytes"], "hbm_write_bytes": r["hbm_write_bytes"],
-                         "pmc_avg_ns": r.get("pmc_avg_ns")}
-    ent["source"] = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 2 ({root}); "
-                     "read bytes = 2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md HBM)")
-    data[tag] = ent
+            if name in kernels:  # two instantiations of one role in one run: keep the busier one
+                if kernels[name]["pmc_avg_ns"] and (r.get("pmc_avg_ns") or 0) <= kernels[name]["pmc_avg_ns"]:
+                    continue
+            kernels[name] = {"symbol": k, "hbm_read_bytes": r["hbm_read_bytes"], "hbm_write_bytes": r["hbm_write_bytes"],
+                             "pmc_avg_ns": r.get("pmc_avg_ns")}
+    data[tag] = {"source_hash": src_hash, "kernels": kernels,
+                 "source": (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 2 ({root}); "
+                            "read bytes = 2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md HBM)")}
     json.dump(data, open(tj, "w"), indent=1)
     print("wrote", tj)
