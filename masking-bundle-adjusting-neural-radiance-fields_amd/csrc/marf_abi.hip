@@ -74,16 +74,18 @@ struct marf_net {
     int pipe_mode, pipe_wg, pipe_piece;  // pipelined weight gradients (marf_net_set_pipeline)
 };
 
-// MARF_DIAG_PREC = "WTAD,WTAD,..." per layer (digits: marf_common.h diag_round modes; the last entry
-// repeats): the rounding a lower-precision recipe would apply, emulated by the fp32 kernels of a
-// MARF_DIAG_RT build (tools/recipe_sweep.sh).  Read once at net creation; other builds ignore it.
+// MARF_DIAG_PREC = "WTAD[S],WTAD,..." per layer (digits: marf_common.h diag_round modes; the last
+// entry repeats): the rounding a lower-precision recipe would apply, emulated by the fp32 kernels of
+// a MARF_DIAG_RT build (tools/recipe_sweep.sh); an optional fifth digit of the first entry rounds
+// every saved tensor the weight gradients read (feat_l, dz_l).  Read once at net creation; other
+// builds ignore it.
 static void parse_diag(marf_net* n) {
     const char* e = getenv("MARF_DIAG_PREC");
     unsigned code = 0;
     for (int l = 0; l < n->n_layers; ++l) {
         if (e && *e) {
             code = 0;
-            for (int k = 0; k < 4 && e[k] >= '0' && e[k] <= '9'; ++k) code |= (unsigned)(e[k] - '0') << (4 * k);
+            for (int k = 0; k < 5 && e[k] >= '0' && e[k] <= '9'; ++k) code |= (unsigned)(e[k] - '0') << (4 * k);
             while (*e && *e != ',') ++e;
             if (*e == ',') ++e;
         }

@@ -78,8 +78,10 @@ MARF_DEV float diag_round(float x, int mode) {
 MARF_DEV int diag_mode(unsigned code, int k) { return (int)((code >> (4 * k)) & 15u); }
 #ifdef MARF_DIAG_RT
 #define MARF_DIAG_ROUND(x, code, k) diag_round((x), diag_mode((code), (k)))
+#define MARF_DIAG_SAVE(net) diag_mode((net).diag[0], 4)  // saved-tensor rounding (fifth digit)
 #else
 #define MARF_DIAG_ROUND(x, code, k) (x)
+#define MARF_DIAG_SAVE(net) 0
 #endif
 
 // ------------------------------------------------------------------ precision traits

@@ -14,7 +14,8 @@
 namespace marf {
 
 template <class P>
-MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int cols, typename P::T* dst, int ldd) {
+MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int cols, typename P::T* dst, int ldd,
+                            int rmode = 0) {
     // LDS [rows][lda] -> global [rows][ldd], first `cols` columns. bf16: 16-byte chunks.
     // The (row, chunk) walk is incremental: one division per call, none per element.
     typedef typename P::T T;
@@ -35,7 +36,7 @@ MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int col
     } else {
         for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
             int r = e / cols, c = e - r * cols;
-            dst[(size_t)r * ldd + c] = act[(size_t)r * lda + c];
+            dst[(size_t)r * ldd + c] = rmode ? diag_round(act[(size_t)r * lda + c], rmode) : act[(size_t)r * lda + c];
         }
     }
 }
@@ -311,12 +312,12 @@ MARF_DEV void tile_origin(const GeoDev& g, int tile, int TP, int& b, int& p0, lo
 // gemm_tile), fp32 tiles (unaligned LDS rows) are copied right away (job left idle).
 template <class P, int NW = 4>
 MARF_DEV void save_tile(TileStore<typename P::T>& job, const typename P::T* act, int lda, int rows, int cols,
-                        typename P::T* dst, int nk_next) {
+                        typename P::T* dst, int nk_next, int rmode = 0) {
     if constexpr (sizeof(typename P::T) == 2) {
         const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         job.init(lda, dst, cols, rows, cols, wave, lane, NW);
     } else {
-        copy_tile_out<P>(act, lda, rows, cols, dst, cols);
+        copy_tile_out<P>(act, lda, rows, cols, dst, cols, rmode);  // (rmode: MARF_DIAG_RT experiments)
         job.clear();
     }
 }

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
     // every saved tile streams out during the GEMM that reads it next (TileStore)
     TileStore<T> st;
     save_tile<P, NW>(st, act, lda, TP, net.Kp[0], SAVE_DST(reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0]),
-                     net.Kp[0] / P::KS);
+                     net.Kp[0] / P::KS, MARF_DIAG_SAVE(net));
 
     // ---- hidden layers (forward); the last one is peeled so the last layer's weight fragments
     //      can be in flight behind its epilogue without pinning registers through the loop
@@ -128,7 +128,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
         if (l < 3) STAMP(3 + 2 * l);
         st.clear();
         if (l + 1 < nl - 1)  // the last layer's input never leaves LDS
-            save_tile<P, NW>(st, act, lda, TP, M, SAVE_DST(reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M), M / P::KS);
+            save_tile<P, NW>(st, act, lda, TP, M, SAVE_DST(reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M), M / P::KS,
+                            MARF_DIAG_SAVE(net));
     };
     for (int l = 0; l < nl - 2; ++l) hidden(l);
     constexpr int NWL = 8;  // prefetched last-layer k-steps (16x16 fragments)
@@ -310,7 +311,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
         mask_epilogue<P, RT, PT, NW>(acc, act, lda, n_rt, wave, lane, mw, net.diag[l - 1]);
         __syncthreads();
         if (l <= 4) STAMP(15 - l);  // 14 .. 11
-        save_tile<P, NW>(st, act, lda, TP, R, SAVE_DST(reinterpret_cast<T*>(a.dz[l]) + slot0 * R, R), net.Mt[l - 1] / P::KS);
+        save_tile<P, NW>(st, act, lda, TP, R, SAVE_DST(reinterpret_cast<T*>(a.dz[l]) + slot0 * R, R), net.Mt[l - 1] / P::KS,
+                         MARF_DIAG_SAVE(net));
     }
 
     // ---- layer-0 dgrad + posenc / warp adjoint -> dH partial

@@ -220,17 +220,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
 // Issued as inline asm: hipcc tracks its own builtin LDS-DMA and waits vmcnt(0) before the next
 // ds_read of the same LDS array, which would drain the ring; the asm form is outside its
 // bookkeeping, and the kernel counts completion itself.  lds: wave-uniform LDS byte address.
-#ifndef MARF_WG_NT
-#define MARF_WG_NT 0
-#endif
-#if MARF_WG_NT
-#define MARF_WG_POL " nt"
-#else
-#define MARF_WG_POL ""
-#endif
 MARF_DEV void glds16(const char* src, unsigned lds) {
     unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" MARF_WG_POL "\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(src), "s"(lds)
                  : "memory");
@@ -661,25 +653,18 @@ static bool wgrad_dma_enabled() {
     return !(e && e[0] == '0');
 }
 
-#ifndef MARF_WG_NBUF_H
-#define MARF_WG_NBUF_H 4
-#endif
-#ifndef MARF_WG_NBUF_0
-#define MARF_WG_NBUF_0 4
-#endif
-#ifndef MARF_WG_SP0
-#define MARF_WG_SP0 64
-#endif
-#ifndef MARF_WG_SPH
-#define MARF_WG_SPH 32
-#endif
+// Ring shapes (same-box A/B, profiles/r4g, r4h): the hidden layers read 32-row stages of dz + feat
+// through a 4-deep ring (64-row stages, a 5-deep ring and non-temporal loads measured no faster);
+// the layer-0 gradient, which recomputes feat_0 and moves only dz over the ring, runs 64-row stages
+// 3 deep (0.65 -> 0.53 ms at C3: half the barriers per pixel).
+constexpr int WG_SPH = 32, WG_NBUF_H = 4, WG_SP0 = 64, WG_NBUF_0 = 3, WG_NBUF_96 = 4;
 
 template <class P, int KF, bool F0 = false>
 static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
     a.n_chunks = n_chunks;
     a.n_oblk_c = a.K / KF;
-    constexpr int SP = F0 ? MARF_WG_SP0 : KF == 256 ? MARF_WG_SPH : 32;
-    constexpr int NBUF = KF == 256 ? (SP == 64 ? 2 : MARF_WG_NBUF_H) : (SP == 64 ? 3 : MARF_WG_NBUF_0);  // ring depth within 160 KB of LDS
+    constexpr int SP = F0 ? WG_SP0 : KF == 256 ? WG_SPH : 32;
+    constexpr int NBUF = KF == 256 ? WG_NBUF_H : F0 ? WG_NBUF_0 : WG_NBUF_96;  // ring depth within 160 KB of LDS
     const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024) + (F0 ? (9 * F0_PATCHES + 32 + (NBUF + 1) * SP * 2) * 4 : 0);
     {
         hipError_t e = ensure_dynamic_lds((const void*)k_wgrad_dma<P, NBUF, SP, KF, F0>, lds);
@@ -724,7 +709,7 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
     // LDS-DMA ring: 256-wide dz with a 256-wide (hidden) or 96-wide (layer 0, L = 16) feat
     const bool dma = M % 256 == 0 && ldz % 8 == 0 && ldz >= M && S % 32 == 0 && chunk % 32 == 0 &&
                      (long long)n_chunks * (M / 256) * ((K + 255) / 256) <= 0x7fffffff && wgrad_dma_enabled();
-    const bool dma256 = dma && K % 256 == 0 && ldf % 8 == 0 && ldf >= K && S % MARF_WG_SPH == 0 && chunk % MARF_WG_SPH == 0,
+    const bool dma256 = dma && K % 256 == 0 && ldf % 8 == 0 && ldf >= K && S % WG_SPH == 0 && chunk % WG_SPH == 0,
                dma96 = dma && K == 96 && ldf == 96;
     if (rng && (dtype == 0 || !(dma256 || dma96))) return hipErrorInvalidValue;  // range mode: LDS-DMA kernel only
     if (dtype == 1) {
@@ -760,7 +745,7 @@ bool marf_wgrad_range_ok(int dtype, int M, int ldz, int K, int ldf) {
 // Layer-0 weight gradient with feat_0 recomputed on chip (step kernel's feat0_recompute); bf16,
 // 256-wide layer 0, the 96-wide feat_0 of L = 13..16.  False if the shape does not qualify.
 bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk, int n_chunks, long long Np_pad) {
-    return M == 256 && ldz % 8 == 0 && ldz >= M && ldf0 == 96 && S % MARF_WG_SP0 == 0 && chunk % MARF_WG_SP0 == 0 &&
+    return M == 256 && ldz % 8 == 0 && ldz >= M && ldf0 == 96 && S % WG_SP0 == 0 && chunk % WG_SP0 == 0 &&
            (long long)n_chunks <= 0x7fffffff && Np_pad < (1 << 24) && (chunk + Np_pad - 1) / Np_pad + 1 <= F0_PATCHES;
 }
 

@@ -6,7 +6,7 @@ for round in 1 2; do
   for spec in "$@"; do
     name=${spec%%=*}; rest=${spec#*=}; envs=${rest%%|*}; lib=${rest#*|}
     if [ -n "$lib" ]; then L="MARF_LIB=$PWD/masking-bundle-adjusting-neural-radiance-fields_amd/lib/$lib"; else L=""; fi
-    env $envs $L timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render > gpurun_out/ab_${TAG}_${name}_$round.json 2> gpurun_out/ab_${TAG}_${name}_$round.err || { echo "$name failed"; tail -3 gpurun_out/ab_${TAG}_${name}_$round.err; exit 1; }
+    env $envs $L timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render $AB_ARGS > gpurun_out/ab_${TAG}_${name}_$round.json 2> gpurun_out/ab_${TAG}_${name}_$round.err || { echo "$name failed"; tail -3 gpurun_out/ab_${TAG}_${name}_$round.err; exit 1; }
     python -c "
 import json; d=json.loads(open('gpurun_out/ab_${TAG}_${name}_$round.json').read().strip().splitlines()[-1])
 kk = d.get('kernels', {}); wg = ' '.join('%s %.3f' % (k, v['avg_ms']) for k, v in sorted(kk.items()) if k.startswith('wgrad'))
