@@ -960,10 +960,12 @@ static void plan_pipe(const marf_net* n, const GeoDev& g, long long S, int n_til
     pp.n_parts = (P - 1) * R + cus;
 }
 
-// the second stream and the events of the pipeline, per device (created once)
+// the second stream and the events of the pipeline, per device (created once); `use` is held by a
+// caller across its whole record / wait sequence, so two host threads never interleave on the events
 struct PipeStreams {
     hipStream_t s2;
     hipEvent_t ev[MARF_PIPE_MAXP + 1];
+    std::mutex use;
 };
 static int pipe_streams(PipeStreams** out) {
     static std::mutex mu;
@@ -1185,6 +1187,7 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
         PipeStreams* st = nullptr;
         rc = pipe_streams(&st);
         if (rc) return rc;
+        std::lock_guard<std::mutex> hold(st->use);
         float* const blast0 = a.blast_partial;
         float* const wlast0 = a.wlast_partial;
         for (int j = 0; j < pp.P; ++j) {

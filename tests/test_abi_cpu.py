@@ -70,3 +70,50 @@ def test_product_refuses_cpu_tensors(lib):
     import marf_hip
     with pytest.raises(RuntimeError, match="ROCm GPU"):
         marf_hip.sl3_to_SL3(torch.zeros(2, 8))
+
+
+def test_split_recipe_kernel_choice_by_size(lib, monkeypatch):
+    """marf_net_create_hint: the split recipe runs k_step3 below 48 block tiles of 128 pixels per CU
+    and k_step2 above (no GPU here: 256 CUs assumed, as on MI355X); MARF_STEP3 forces either; the
+    other recipes keep their kernels."""
+    import marf_hip
+    monkeypatch.delenv("MARF_STEP3", raising=False)
+    dims = [66, 256, 256, 256, 256, 3]
+    c1 = 5 * 180 * 240
+    c3 = 64 * 256 * 256
+    edge = 48 * 128 * 256
+    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=c1).step_kernel == "k_step3"
+    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=edge - 1).step_kernel == "k_step3"
+    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=edge).step_kernel == "k_step2"
+    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=c3).step_kernel == "k_step2"
+    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3).step_kernel == "k_step2"  # size unknown
+    monkeypatch.setenv("MARF_STEP3", "1")
+    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=c3).step_kernel == "k_step3"
+    monkeypatch.setenv("MARF_STEP3", "0")
+    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=c1).step_kernel == "k_step2"
+    monkeypatch.delenv("MARF_STEP3")
+    assert marf_hip.Net(dims, 16, marf_hip.MARF_FP32, pixels_hint=c1).step_kernel == "k_mlp_step"
+    spans = marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3).layer_spans
+    assert spans[0] == (0, 256 * 66 + 256) and sum(n for _, n in spans) == 215299
+
+
+def test_bench_traffic_only_from_the_loaded_library(lib, tmp_path, monkeypatch):
+    """bench.py reports PMC traffic only for an entry measured on the library it runs (same
+    marf_source_hash) and on the same kernel (symbol prefix); anything else is null."""
+    import json
+    import sys
+    import marf_hip
+    sys.path.insert(0, ROOT)
+    import bench
+    have = marf_hip.lib().marf_source_hash().decode()
+    (tmp_path / "profiles").mkdir()
+    entry = {"source_hash": have, "source": "test", "kernels": {
+        "mlp_step": {"symbol": "k_step2<256, true, 4, 4>", "hbm_read_bytes": 1.0, "hbm_write_bytes": 2.0, "pmc_avg_ns": 1.0}}}
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({"c3/bf16x3": entry}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.pmc_traffic("c3", "bf16x3", "mlp_step", "k_step2")[0] == 3.0
+    assert bench.pmc_traffic("c3", "bf16x3", "mlp_step", "k_step3") is None     # another kernel
+    assert bench.pmc_traffic("c3", "bf16", "mlp_step", "k_step2") is None       # no entry
+    entry["source_hash"] = "0" * 40
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({"c3/bf16x3": entry}))
+    assert bench.pmc_traffic("c3", "bf16x3", "mlp_step", "k_step2") is None     # another build
