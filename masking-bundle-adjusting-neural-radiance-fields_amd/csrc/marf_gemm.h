@@ -88,9 +88,7 @@ struct TileStore {
     }
     MARF_DEV void write(uint4 v) {
         constexpr int VEC = 16 / sizeof(T);
-#ifndef MARF_DIAG_NO_SAVE
         *reinterpret_cast<uint4*>(dst + (size_t)row() * ldd + VEC * lc) = v;
-#endif
         ++q;
     }
     MARF_DEV void flush(const T* src) {

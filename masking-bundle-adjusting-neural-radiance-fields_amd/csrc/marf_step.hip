@@ -32,14 +32,6 @@ MARF_DEV i16x4 tr_read16(const u16* p) {
 
 #define STAMP(i) MARF_STAMP(sp, i)
 
-// Diagnostic (MARF_DIAG_STORE_L2): every block writes its saved tiles into one of 64 small regions
-// at the start of dz_1 (<= 64 * TP * 512 elements, L2-resident) instead of its own rows.
-#ifdef MARF_DIAG_STORE_L2
-#define SAVE_DST(ptr, cols) (reinterpret_cast<T*>(a.dz[1]) + (size_t)(blockIdx.x & 63) * TP * (cols))
-#else
-#define SAVE_DST(ptr, cols) (ptr)
-#endif
-
 // BL: every forward bias staged in LDS at the start (sum of the hidden widths <= MARF_STEP_NBIAS):
 // a GEMM's accumulator init reads LDS instead of loading from global behind the previous GEMM's
 // stores (vmcnt retires in issue order), and no bias registers are live across the prologue.
@@ -106,7 +98,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
     STAMP(1);
     // every saved tile streams out during the GEMM that reads it next (TileStore)
     TileStore<T> st;
-    save_tile<P, NW>(st, act, lda, TP, net.Kp[0], SAVE_DST(reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0], net.Kp[0]),
+    save_tile<P, NW>(st, act, lda, TP, net.Kp[0], reinterpret_cast<T*>(a.feat[0]) + slot0 * net.Kp[0],
                      net.Kp[0] / P::KS, MARF_DIAG_SAVE(net));
 
     // ---- hidden layers (forward); the last one is peeled so the last layer's weight fragments
@@ -128,7 +120,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
         if (l < 3) STAMP(3 + 2 * l);
         st.clear();
         if (l + 1 < nl - 1)  // the last layer's input never leaves LDS
-            save_tile<P, NW>(st, act, lda, TP, M, SAVE_DST(reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M), M / P::KS,
+            save_tile<P, NW>(st, act, lda, TP, M, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M / P::KS,
                             MARF_DIAG_SAVE(net));
     };
     for (int l = 0; l < nl - 2; ++l) hidden(l);
@@ -311,7 +303,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
         mask_epilogue<P, RT, PT, NW>(acc, act, lda, n_rt, wave, lane, mw, net.diag[l - 1]);
         __syncthreads();
         if (l <= 4) STAMP(15 - l);  // 14 .. 11
-        save_tile<P, NW>(st, act, lda, TP, R, SAVE_DST(reinterpret_cast<T*>(a.dz[l]) + slot0 * R, R), net.Mt[l - 1] / P::KS,
+        save_tile<P, NW>(st, act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, net.Mt[l - 1] / P::KS,
                          MARF_DIAG_SAVE(net));
     }
 
