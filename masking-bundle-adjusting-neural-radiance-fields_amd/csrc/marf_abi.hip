@@ -1089,7 +1089,12 @@ static int wgrad_piece(const marf_net* net, const GeoDev& g, const Step2BufPlan&
 
 static hipError_t launch_s2(const marf_net* n, const Step2Args& a, int grid, hipStream_t s) {
     const Step2NetPlan& q = n->s2;
-    if (q.variant != 3) return marf_launch_step2(a, q.variant, grid, s);
+    if (q.variant != 3) {
+        // the compile-time layer-0 instantiation: split recipe, every hidden layer 256 wide, L = 13..16
+        bool full = q.variant == 1 && q.nk0 == 5 && q.r0 == 3;
+        for (int l = 0; l < n->n_layers - 1; ++l) full = full && n->Mp[l] == 256;
+        return marf_launch_step2(a, q.variant, grid, s, full ? q.nk0 : 0);
+    }
     bool full = n->L >= 1;  // every hidden layer 256 wide
     for (int l = 0; l < n->n_layers - 1; ++l) full = full && n->Mp[l] == 256;
     return marf_launch_step3(a, full, q.NW, grid, s);

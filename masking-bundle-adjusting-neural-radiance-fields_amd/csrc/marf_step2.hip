@@ -153,10 +153,17 @@ struct S2Cfg {
     static_assert(PER_DMA * NW * 1024 == SLOT, "slot size");
 };
 
-template <int HM, bool SPLIT, int NW, int MAXR>
+// NK0F: 0 = the generic instantiation (layer-0 k-steps, row tiles per stage and layer widths read at
+// run time); > 0 = a full-width net (every hidden layer HM wide) with NK0F layer-0 k-steps, whose
+// layer-0 stages, GEMM lengths and row-tile counts are compile-time (no live-k-step branches)
+template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0>
 __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     typedef S2Cfg<HM, SPLIT, NW, MAXR> C;
     constexpr int NKH = C::NKH, NRT = C::NRT, NS = C::NS;
+    constexpr bool FIX = NK0F > 0;
+    static_assert(NK0F <= C::NK0, "layer-0 k-steps");
+    constexpr int R0Q = NKH / (FIX ? NK0F : NKH);  // layer-0 row tiles per stage (the host's r0)
+    constexpr int R0F = R0Q < 1 ? 1 : (R0Q > NRT ? NRT : R0Q);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -452,6 +459,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     typedef std::integral_constant<int, SPLIT ? 2 : 0> MBt;
     typedef std::integral_constant<int, NKH> NKHt;
     typedef std::integral_constant<int, C::NK0> NK0t;
+    // layer 0's GEMM length: compile-time NK0F (every k-step live) or NK0 with a run-time count
+    typedef std::conditional_t<FIX, std::integral_constant<int, FIX ? NK0F : 1>, NK0t> NK0x;
+    const int nk0 = FIX ? NK0F : a.nk0, r0 = FIX ? R0F : a.r0;
     typedef std::integral_constant<int, 1> NK1t;
 
     auto bias_init = [&](int boff, int rt) -> f32x16 {
@@ -664,7 +674,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const float cd = h ? v : u;
             S2Frag F0h[C::NK0], F0l[C::NK0];
             {
-                const int ng = a.nk0 - 1;  // band groups of 4
+                const int ng = nk0 - 1;  // band groups of 4
 #pragma unroll
                 for (int g = 0; g < C::NK0 - 1; ++g) {
                     if (g < ng) {
@@ -703,10 +713,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                     u16* row = ly_ptr(0, 0) + myslot * ly_int(0, 3);
 #pragma unroll
                     for (int g = 0; g < C::NK0; ++g)
-                        if (g < a.nk0) s2_st16(row + 16 * g + 8 * h, F0h[g].u);
-                    st_cur += a.nk0;
-                    if (16 * a.nk0 < ly_int(0, 3)) {
-                        s2_st16(row + 16 * a.nk0 + 8 * h, make_uint4(0, 0, 0, 0));
+                        if (g < nk0) s2_st16(row + 16 * g + 8 * h, F0h[g].u);
+                    st_cur += nk0;
+                    if (16 * nk0 < ly_int(0, 3)) {
+                        s2_st16(row + 16 * nk0 + 8 * h, make_uint4(0, 0, 0, 0));
                         st_cur += 1;
                     }
                 }
@@ -721,7 +731,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 constexpr int MS = decltype(ms_tag)::value;  // epilogue micro-steps beside each k-step
                 typedef std::integral_constant<bool, decltype(nk_tag)::value == NKH> PcL;  // hidden: pieces in the GEMM
                 constexpr bool SPLITPK = SPLIT && MS == 1 && decltype(nk_tag)::value == NKH;  // hidden, split recipe
-                const int nrt = ly_int(l, 0);
+                const int nrt = FIX ? NRT : ly_int(l, 0);
                 const bool save = l + 1 < nl - 1 && !a.fwd_only;
                 u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) + 8 * h : nullptr;
                 const int boff = ly_int(l, 2);
@@ -732,13 +742,13 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                     f32x16& prv = (rt & 1) ? acc0 : acc1;
                     if (rt < nrt) {
                         // layer 0: r0 row tiles share a stage (their few k-steps fill one slot)
-                        const int sub = l == 0 ? rt % a.r0 : 0;
+                        const int sub = l == 0 ? rt % r0 : 0;
                         // the bias (a static LDS table) before the stage wait: its reads overlap it
                         S2T_BEGIN(15);
                         cur = bias_init(boff, rt);
                         S2T_END(15);
                         if (sub == 0) slot0 = stage_begin(l == 0);  // layer 0: the pieces in a burst
-                        const char* slot = slot0 + sub * a.nk0 * 1024;
+                        const char* slot = slot0 + sub * nk0 * 1024;
                         // the next tile's target / mask / H into the other input buffer (the tile that
                         // read it last finished before this stage's barrier)
                         if (l == 0 && rt == 0 && ti + 1 < my_tiles) issue_pro(tile + (int)gridDim.x, pb ^ 1);
@@ -792,15 +802,15 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         zero_out(Oh[2 * rt], Oh[2 * rt + 1], Ol[2 * rt], Ol[2 * rt + 1]);
                     }
                 });
-                S2T_BEGIN(14);
 #pragma unroll
                 for (int k = 0; k < NKH; ++k) {
                     Bh[k] = Oh[k];
                     if constexpr (SPLIT) Bl[k] = Ol[k];
                 }
-                S2T_END(14);
             };
-            fwd_layer(0, F0h, F0l, a.nk0, NK0t(), std::integral_constant<int, 2>());
+            S2T_BEGIN(14);  // (phase stamps: layer 0 on its own)
+            fwd_layer(0, F0h, F0l, nk0, NK0x(), std::integral_constant<int, 2>());
+            S2T_END(14);
             for (int l = 1; l < nl - 1; ++l) fwd_layer(l, Bh, Bl, NKH, NKHt(), std::integral_constant<int, 1>());
 
             S2T_END(5);
@@ -942,7 +952,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         //      row tile's single k-step (tile rt at rt KB)
         {
             const int lmask = nl - 2;
-            const int nrt = ly_int(nl - 1, 1);
+            const int nrt = FIX ? NRT : ly_int(nl - 1, 1);
             u16* brow[NS];
             s2_sfor<NS>([&](auto sc) {
                 brow[decltype(sc)::value] = ly_ptr(nl - 1, 1) + myslot_of(decltype(sc)::value) * ly_int(nl - 1, 4) + 8 * h;
@@ -993,7 +1003,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         // ---- hidden dgrad chain l = nl-2 .. 1
         for (int l = nl - 2; l >= 1; --l) {
             const int lmask = l - 1;
-            const int nrt = ly_int(l, 1);
+            const int nrt = FIX ? NRT : ly_int(l, 1);
             u16* brow[NS];
             s2_sfor<NS>([&](auto sc) {
                 brow[decltype(sc)::value] = ly_ptr(l, 1) + myslot_of(decltype(sc)::value) * ly_int(l, 4) + 8 * h;
@@ -1336,20 +1346,24 @@ __global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog
 
 using namespace marf;
 
-template <int HM, bool SPLIT, int NW, int MAXR>
+template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0>
 static hipError_t launch_step2_t(const Step2Args& a, int grid, hipStream_t s) {
-    hipError_t e = ensure_dynamic_lds((const void*)k_step2<HM, SPLIT, NW, MAXR>, (size_t)a.lds_total);
+    hipError_t e = ensure_dynamic_lds((const void*)k_step2<HM, SPLIT, NW, MAXR, NK0F>, (size_t)a.lds_total);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_step2<HM, SPLIT, NW, MAXR>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
+    hipLaunchKernelGGL((k_step2<HM, SPLIT, NW, MAXR, NK0F>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
     return hipGetLastError();
 }
 
 // variant: 0 = plain bf16, 256-wide, 8 waves; 1 = split bf16, 256-wide, 4 waves; 2 = plain bf16,
 // 256-wide, 4 waves (diagnostic: the variant-0 arithmetic at one wave per SIMD)
-hipError_t marf_launch_step2(const Step2Args& a, int variant, int grid, hipStream_t s) {
+// full_nk0: a full-width net's layer-0 k-step count (its r0 and row-tile counts follow from it; see
+// k_step2's NK0F), or 0 for the generic instantiation
+hipError_t marf_launch_step2(const Step2Args& a, int variant, int grid, hipStream_t s, int full_nk0) {
     switch (variant) {
         case 0: return launch_step2_t<256, false, 8, 4>(a, grid, s);
-        case 1: return launch_step2_t<256, true, 4, 4>(a, grid, s);
+        case 1:
+            if (full_nk0 == 5) return launch_step2_t<256, true, 4, 4, 5>(a, grid, s);  // L = 13..16
+            return launch_step2_t<256, true, 4, 4>(a, grid, s);
         case 2: return launch_step2_t<256, false, 4, 4>(a, grid, s);  // diagnostic: bf16 on 4 waves
         default: return hipErrorInvalidValue;
     }

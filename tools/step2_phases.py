@@ -18,7 +18,7 @@ NAMES = ["stage wait+barrier", "DMA issue", "backward (BWL..BW0)", "dH tail", "p
          "last layer + dW_last", "tile loop total", "  in fwd GEMM bodies", "  in dgrad GEMM bodies",
          "  fwd tile finish (frag regs, mask, stores)", "  dgrad tile finish (frag regs, stores)",
          "  stage vmcnt/lgkmcnt wait (of wait+barrier)", "  fwd epilogue steps outside GEMM bodies",
-         "  fwd operand copies (B = O)", "  fwd bias init"]
+         "  forward layer 0 (of forward)", "  fwd bias init"]
 
 
 NAMES3 = ["stage vmcnt/lgkmcnt wait", "barrier", "DMA issue", "prologue", "forward layer 0", "forward hidden layers",
@@ -34,6 +34,7 @@ def main():
                     help="step3: the two-waves-per-SIMD kernel (marf_step3.hip, MARF_STEP3=1)")
     args = ap.parse_args()
     names, total_col = (NAMES3, 15) if args.kernel == "step3" else (NAMES, 7)
+    os.environ["MARF_STEP3"] = "1" if args.kernel == "step3" else "0"  # (C3's size alone picks k_step2)
     import marf_hip
     from model import planar
     from util import EasyDict as edict
