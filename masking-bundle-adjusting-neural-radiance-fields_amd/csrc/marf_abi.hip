@@ -150,10 +150,19 @@ static void plan_step3_net(marf_net* n) {
 
 // Which pixel-per-wave variant (marf_step2.hip) runs this net, its weight-program shape and the
 // byte layout of the program / bias table / layer-0 column map appended to the packed buffer.
-// The split recipe has two kernels of identical arithmetic (k_step3 = k_step2 bit for bit): k_step3
-// (two waves per SIMD) is the faster one below about 48 block tiles of 128 pixels per CU (C1: 6.6,
-// -10 % kernel time), k_step2 above it (C3: 128, k_step3 +4 %); pixels_hint (the step's pixels per
-// GPU, 0 = unknown) picks it, MARF_STEP3=0 / 1 at net creation forces one.
+// The split recipe has two kernels of identical arithmetic (k_step3 = k_step2 bit for bit). k_step2's
+// compile-time instantiations (full-width nets at L = 8, 9..12, 15, 16) are the faster ones at every
+// size measured (C3-shaped batches of 4..64 patches 10-12 %, C1 6 %: profiles/r4s); otherwise
+// k_step3 (two waves per SIMD) wins below about 48 block tiles of 128 pixels per CU (C1: 6.6 tiles,
+// -10 % against the generic k_step2) and loses above (C3: +4 %).  pixels_hint (the step's pixels per
+// GPU, 0 = unknown) picks; MARF_STEP3=0 / 1 at net creation forces one.
+static bool step2_specialized(const marf_net* n) {
+    const int nl = n->n_layers, L = n->L;
+    for (int l = 0; l < nl - 1; ++l)
+        if (n->Mp[l] != 256) return false;
+    const int nk0 = (L + 3) / 4 + 1, nta = (2 * L + 1 + 15) / 16;
+    return n->Kp[nl - 1] == 256 && ((nk0 == 5 && nta == 3) || (nk0 == 4 && nta == 2) || (nk0 == 3 && nta == 2));
+}
 static void plan_step2_net(marf_net* n, long long pixels_hint) {
     Step2NetPlan& q = n->s2;
     memset(&q, 0, sizeof(q));
@@ -170,7 +179,8 @@ static void plan_step2_net(marf_net* n, long long pixels_hint) {
     if (q.variant == 1) {
         const char* e = getenv("MARF_STEP3");
         const bool step3 = (e && e[0]) ? e[0] == '1'
-                                       : pixels_hint > 0 && pixels_hint < 48LL * 128 * device_cus();
+                                       : !step2_specialized(n) && pixels_hint > 0 &&
+                                             pixels_hint < 48LL * 128 * device_cus();
         if (step3) {
             plan_step3_net(n);
             return;
@@ -1090,8 +1100,9 @@ static int wgrad_piece(const marf_net* net, const GeoDev& g, const Step2BufPlan&
 static hipError_t launch_s2(const marf_net* n, const Step2Args& a, int grid, hipStream_t s) {
     const Step2NetPlan& q = n->s2;
     if (q.variant != 3) {
-        // the compile-time layer-0 instantiation: split recipe, every hidden layer 256 wide, L = 13..16
-        bool full = q.variant == 1 && q.nk0 == 5 && q.r0 == 3;
+        // the compile-time layer-0 instantiations: split recipe, every hidden layer 256 wide, the
+        // layer-0 row tiles per stage the kernel derives from nk0, a 256-wide last-layer input
+        bool full = q.variant == 1 && q.nk0 >= 1 && q.r0 == std::max(1, std::min(8, 16 / q.nk0)) && q.Kl == 256;
         for (int l = 0; l < n->n_layers - 1; ++l) full = full && n->Mp[l] == 256;
         return marf_launch_step2(a, q.variant, grid, s, full ? q.nk0 : 0);
     }

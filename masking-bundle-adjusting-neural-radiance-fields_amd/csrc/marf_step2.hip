@@ -154,9 +154,10 @@ struct S2Cfg {
 };
 
 // NK0F: 0 = the generic instantiation (layer-0 k-steps, row tiles per stage and layer widths read at
-// run time); > 0 = a full-width net (every hidden layer HM wide) with NK0F layer-0 k-steps, whose
-// layer-0 stages, GEMM lengths and row-tile counts are compile-time (no live-k-step branches)
-template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0>
+// run time); > 0 = a full-width net (every hidden layer HM wide) with NK0F layer-0 k-steps and NTAF
+// adjoint row tiles, whose layer-0 stages, GEMM lengths and row-tile counts are compile-time (no
+// live-k-step branches; 10.4 -> 9.5 ms at C3, profiles/r4r)
+template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0, int NTAF = 0>
 __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     typedef S2Cfg<HM, SPLIT, NW, MAXR> C;
     constexpr int NKH = C::NKH, NRT = C::NRT, NS = C::NS;
@@ -882,7 +883,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 }
                 const bf16x8 ga = *reinterpret_cast<const bf16x8*>(gts + (lane & 15) * 32 + 8 * (lane >> 4));
                 const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-                const int nkl = a.Kl / 16;
+                const int nkl = FIX ? NKH : a.Kl / 16;
+                const int Klw = FIX ? HM : a.Kl;
 #pragma unroll
                 for (int ks = 0; ks < NKH; ++ks) {
                     if (ks < nkl) {
@@ -895,7 +897,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         for (int c = 0; c < 3; ++c) lo[c] = __shfl_down(r4[c], 16, 64);
                         if (lane < 16) {
 #pragma unroll
-                            for (int c = 0; c < 3; ++c) wla[c * a.Kl + 16 * ks + lane] += r4[c] + lo[c];
+                            for (int c = 0; c < 3; ++c) wla[c * Klw + 16 * ks + lane] += r4[c] + lo[c];
                         }
                     }
                 }
@@ -1061,7 +1063,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             cds[s] = h ? ss[s].X1 / dd : ss[s].X0 / dd;
         });
         {
-            const int nta = a.nta;
+            const int nta = FIX ? NTAF : a.nta;
             auto adj_band = [&](float& d, const float cd, const f32x16& pa, int t, auto ic) {
                 constexpr int i = decltype(ic)::value;
                 const int k = 8 * t + i;
@@ -1346,23 +1348,26 @@ __global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog
 
 using namespace marf;
 
-template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0>
+template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0, int NTAF = 0>
 static hipError_t launch_step2_t(const Step2Args& a, int grid, hipStream_t s) {
-    hipError_t e = ensure_dynamic_lds((const void*)k_step2<HM, SPLIT, NW, MAXR, NK0F>, (size_t)a.lds_total);
+    hipError_t e = ensure_dynamic_lds((const void*)k_step2<HM, SPLIT, NW, MAXR, NK0F, NTAF>, (size_t)a.lds_total);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_step2<HM, SPLIT, NW, MAXR, NK0F>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
+    hipLaunchKernelGGL((k_step2<HM, SPLIT, NW, MAXR, NK0F, NTAF>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
     return hipGetLastError();
 }
 
 // variant: 0 = plain bf16, 256-wide, 8 waves; 1 = split bf16, 256-wide, 4 waves; 2 = plain bf16,
 // 256-wide, 4 waves (diagnostic: the variant-0 arithmetic at one wave per SIMD)
 // full_nk0: a full-width net's layer-0 k-step count (its r0 and row-tile counts follow from it; see
-// k_step2's NK0F), or 0 for the generic instantiation
+// k_step2's NK0F), or 0 for the generic instantiation; the compile-time instantiations cover
+// (nk0, nta) = (5, 3): L = 15, 16; (4, 2): L = 9..12; (3, 2): L = 8
 hipError_t marf_launch_step2(const Step2Args& a, int variant, int grid, hipStream_t s, int full_nk0) {
     switch (variant) {
         case 0: return launch_step2_t<256, false, 8, 4>(a, grid, s);
         case 1:
-            if (full_nk0 == 5) return launch_step2_t<256, true, 4, 4, 5>(a, grid, s);  // L = 13..16
+            if (full_nk0 == 5 && a.nta == 3) return launch_step2_t<256, true, 4, 4, 5, 3>(a, grid, s);
+            if (full_nk0 == 4 && a.nta == 2) return launch_step2_t<256, true, 4, 4, 4, 2>(a, grid, s);
+            if (full_nk0 == 3 && a.nta == 2) return launch_step2_t<256, true, 4, 4, 3, 2>(a, grid, s);
             return launch_step2_t<256, true, 4, 4>(a, grid, s);
         case 2: return launch_step2_t<256, false, 4, 4>(a, grid, s);  // diagnostic: bf16 on 4 waves
         default: return hipErrorInvalidValue;

@@ -73,27 +73,33 @@ def test_product_refuses_cpu_tensors(lib):
 
 
 def test_split_recipe_kernel_choice_by_size(lib, monkeypatch):
-    """marf_net_create_hint: the split recipe runs k_step3 below 48 block tiles of 128 pixels per CU
-    and k_step2 above (no GPU here: 256 CUs assumed, as on MI355X); MARF_STEP3 forces either; the
-    other recipes keep their kernels."""
+    """marf_net_create_hint: the split recipe runs k_step2 wherever one of its compile-time
+    instantiations applies (full-width nets at L = 8, 9..12, 15, 16); otherwise k_step3 below 48
+    block tiles of 128 pixels per CU and k_step2 above (no GPU here: 256 CUs assumed, as on MI355X);
+    MARF_STEP3 forces either; the other recipes keep their kernels."""
     import marf_hip
     monkeypatch.delenv("MARF_STEP3", raising=False)
-    dims = [66, 256, 256, 256, 256, 3]
     c1 = 5 * 180 * 240
     c3 = 64 * 256 * 256
     edge = 48 * 128 * 256
-    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=c1).step_kernel == "k_step3"
-    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=edge - 1).step_kernel == "k_step3"
-    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=edge).step_kernel == "k_step2"
-    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=c3).step_kernel == "k_step2"
-    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3).step_kernel == "k_step2"  # size unknown
+    full16 = [66, 256, 256, 256, 256, 3]
+    for L, dims in ((16, full16), (8, [34, 256, 256, 256, 256, 3]), (10, [42, 256, 256, 256, 256, 3])):
+        for px in (c1, c3, 0):
+            assert marf_hip.Net(dims, L, marf_hip.MARF_BF16X3, pixels_hint=px).step_kernel == "k_step2", (L, px)
+    narrow = [66, 128, 128, 3]  # generic instantiations: the size decides
+    assert marf_hip.Net(narrow, 16, marf_hip.MARF_BF16X3, pixels_hint=c1).step_kernel == "k_step3"
+    assert marf_hip.Net(narrow, 16, marf_hip.MARF_BF16X3, pixels_hint=edge - 1).step_kernel == "k_step3"
+    assert marf_hip.Net(narrow, 16, marf_hip.MARF_BF16X3, pixels_hint=edge).step_kernel == "k_step2"
+    assert marf_hip.Net(narrow, 16, marf_hip.MARF_BF16X3).step_kernel == "k_step2"  # size unknown
+    l13 = [54, 256, 256, 256, 256, 3]  # L = 13: nk0 5 but 2 adjoint tiles, no instantiation
+    assert marf_hip.Net(l13, 13, marf_hip.MARF_BF16X3, pixels_hint=c1).step_kernel == "k_step3"
     monkeypatch.setenv("MARF_STEP3", "1")
-    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=c3).step_kernel == "k_step3"
+    assert marf_hip.Net(full16, 16, marf_hip.MARF_BF16X3, pixels_hint=c3).step_kernel == "k_step3"
     monkeypatch.setenv("MARF_STEP3", "0")
-    assert marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3, pixels_hint=c1).step_kernel == "k_step2"
+    assert marf_hip.Net(narrow, 16, marf_hip.MARF_BF16X3, pixels_hint=c1).step_kernel == "k_step2"
     monkeypatch.delenv("MARF_STEP3")
-    assert marf_hip.Net(dims, 16, marf_hip.MARF_FP32, pixels_hint=c1).step_kernel == "k_mlp_step"
-    spans = marf_hip.Net(dims, 16, marf_hip.MARF_BF16X3).layer_spans
+    assert marf_hip.Net(full16, 16, marf_hip.MARF_FP32, pixels_hint=c1).step_kernel == "k_mlp_step"
+    spans = marf_hip.Net(full16, 16, marf_hip.MARF_BF16X3).layer_spans
     assert spans[0] == (0, 256 * 66 + 256) and sum(n for _, n in spans) == 215299
 
 

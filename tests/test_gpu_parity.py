@@ -815,12 +815,12 @@ def _reference_runs():
     return runs
 
 
-@pytest.mark.parametrize("precision", ["bf16x3", "bf16x3-step2", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16x3", "bf16x3-step3", "fp32"])
 def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path, monkeypatch):
     """BASELINE config 1/2 end to end: the seed=3 cat_batch3 run for 3000 iterations, for the bench
-    recipe on the kernel the library picks at this size (bf16x3: k_step3) and on the other one
-    (bf16x3-step2: k_step2, the kernel bench.py times at C3) -- they compute the same bits
-    (test_step3_bitwise_equals_step2), so they end in the same state -- and for fp32.
+    recipe on the kernel the library picks (bf16x3: k_step2's compile-time L = 8 instantiation, the
+    kernel family bench.py times at C3) and on the other one (bf16x3-step3: k_step3) -- they compute
+    the same bits (test_step3_bitwise_equals_step2), so they end in the same state -- and for fp32.
 
     PSNR: final within 0.05 dB of the reference's 25.9968 dB (north_star).
     Warps: the north_star's 1e-2 cannot be met against a single reference run by the reference
@@ -833,8 +833,8 @@ def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path, monkeypatch):
     is re-rolled by any change of fp32 rounding order, so the kernel the bench times must be the
     kernel whose arithmetic this run pins."""
     monkeypatch.delenv("MARF_STEP3", raising=False)
-    if precision == "bf16x3-step2":
-        monkeypatch.setenv("MARF_STEP3", "0")
+    if precision == "bf16x3-step3":
+        monkeypatch.setenv("MARF_STEP3", "1")
         precision = "bf16x3"
     psnr, warps = _run_c1(precision, tmp_path)
     runs = _reference_runs()
@@ -1024,7 +1024,8 @@ _STEP3_CASES = {
     "c3x2": (2, 256, 16, [256] * 4),              # C3 shape (4), odd layer-0 chunk count (5)
     "c3x3-L10": (3, 256, 10, [256] * 4),          # even layer-0 chunk count (4) (6)
     "L16-1tile": (2, 100, 16, [256] * 4),         # 158 tiles: one tile per block, 98 idle blocks
-    "narrow": (2, 64, 8, [128, 96, 128]),         # the generic instantiation (widths < 256)
+    "narrow": (2, 64, 8, [128, 96, 128]),         # the generic instantiations (widths < 256)
+    "L13": (2, 128, 13, [256] * 4),               # full width, generic k_step2 (nk0 5, 2 adjoint tiles)
 }
 
 
