@@ -42,11 +42,11 @@ MARF_DEV void copy_tile_out(const typename P::T* act, int lda, int rows, int col
 }
 
 // Streams an LDS tile [rows][lda] (first `cols` columns) to global [rows][ldd] in 16-byte chunks
-// while the next GEMM (which reads the same tile) runs: one chunk per lane per k-step, issued
-// branch-free (row and step index clamped, so surplus steps rewrite the last chunk with the same
-// bytes) so the compiler's vmcnt / lgkmcnt bookkeeping stays exact and the weight loads of the
-// ring are never waited for behind a store they do not depend on.  Chunks left over when the
-// GEMM has fewer k-steps than the job flush after it.  bf16 tiles only (16-B aligned LDS rows).
+// right after the GEMM that reads the tile (gemm_tile flushes it there, before the epilogue
+// rewrites the tile).  gemm_rows can also interleave the chunks with its k-steps (JOB 1 / 2), but
+// vmcnt retires in issue order, so a store between the weight-fragment loads makes every later
+// fragment wait for it: measured slower (C5 80.7 vs 66.7 ms), kept only as the JOB template.
+// bf16 tiles only (16-B aligned LDS rows).
 //
 // Wave-uniform walk: rpi = 64 / nch whole rows per wave step (lane -> row lane / nch, chunk
 // lane % nch); wave w of nw copies row groups w, w + nw, ...
@@ -252,33 +252,18 @@ MARF_DEV void gemm_tile(f32x16 (&acc)[RT][PT], const typename P::T* __restrict__
     }
     int na = (n_rt - wave + NW - 1) / NW;
     na = na < 0 ? 0 : (na > RT ? RT : na);
-    // the job's chunks at every k-step, or at every second one when that still covers them
-    const bool half = st.active && 2 * st.nq <= K / P::KS;
-    if (st.active && half) {
-        switch (na) {
-            case 1: gemm_rows<P, 1, RT, PT, 2, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 2: gemm_rows<P, 2, RT, PT, 2, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, 2, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, 2, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            default: st.flush(act); break;
-        }
-    } else if (st.active) {
-        switch (na) {
-            case 1: gemm_rows<P, 1, RT, PT, 1, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 2: gemm_rows<P, 2, RT, PT, 1, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, 1, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, 1, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            default: st.flush(act); break;
-        }
-    } else {
-        switch (na) {
-            case 1: gemm_rows<P, 1, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 2: gemm_rows<P, 2, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
-            default: break;
-        }
+    // The saved tile's stores go out after the GEMM instead of between its weight-fragment loads:
+    // vmcnt retires in issue order, so each fragment wait also waited for the stores issued before
+    // it.  Same bits; C5 (8-wave block) 80.7 -> 66.7 ms, plain bf16 at C3 (4-wave) 5.21 -> 5.07 ms
+    // (profiles/r4w, r4x).  The stores drain during the epilogue, which loads nothing.
+    switch (na) {
+        case 1: gemm_rows<P, 1, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
+        case 2: gemm_rows<P, 2, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
+        case 3: if constexpr (RT >= 3) gemm_rows<P, 3, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
+        case 4: if constexpr (RT >= 4) gemm_rows<P, 4, RT, PT, 0, NW>(acc, W, K, act, lda, wave, lane, st); break;
+        default: break;
     }
+    if (st.active) st.flush(act);
 }
 
 // Store 4 consecutive rows (features) of one accumulator group for this lane's pixel.
