@@ -581,6 +581,25 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         frelu(pa, ec);
         fpack(ec);
     };
+    // The steps E0..15 of an epilogue that run after the GEMM (nothing to hide them beside): the
+    // same operations as frelu / fpack in plain C++, so the compiler interleaves the pairs' chains
+    // (the volatile asm of the in-gap steps keeps each pair's 6-deep chain in program order), then
+    // the mask bits in pair order as mask_pair does.  E0 even.
+    auto fsteps_free = [&](const f32x16& pa, auto e0c) {
+        constexpr int E0 = decltype(e0c)::value;
+        static_assert((E0 & 1) == 0, "whole pairs");
+        uint32_t w[8];
+        s2_sfor<(16 - E0) / 2>([&](auto jc) {
+            constexpr int q = E0 / 2 + decltype(jc)::value;
+            const float x0 = __int_as_float(max(__float_as_int(pa[2 * q]), 0));
+            const float x1 = __int_as_float(max(__float_as_int(pa[2 * q + 1]), 0));
+            const uint32_t hw = s2_pk(x0, x1);
+            w[q] = hw;
+            ep.hw[q] = hw;
+            if constexpr (SPLIT) ep.lw[q] = s2_pk(x0 - s2_lo16(hw), x1 - s2_hi16(hw));
+        });
+        s2_sfor<(16 - E0) / 2>([&](auto jc) { mask_pair(w[E0 / 2 + decltype(jc)::value]); });
+    };
     // forward finish of tile rt: operand fragments of k-steps 2 rt, 2 rt + 1, mask word, 2 stores
     // (last: the layer's last row tile -- an odd row-tile count (a width of 32 mod 64) stores its
     //  mask word without the odd partner's bits)
@@ -619,6 +638,18 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
         } else {
             es.vp = x;
         }
+    };
+    // bstep for all 16 elements at once in plain C++ (the same v_bfe / v_and / v_cvt_pk operations)
+    // for epilogues with no MFMA gaps to hide in: the compiler interleaves the elements' chains
+    auto bsteps_free = [&](EpSt& es, const f32x16& pa, auto rtc) {
+        constexpr int rt = decltype(rtc)::value;
+        s2_sfor<8>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            constexpr int b0 = 16 * 0 + 8 * (1 - (rt & 1)) + 7 - q, b1 = 16 * 1 + 8 * (1 - (rt & 1)) + 7 - q;
+            const float x0 = __int_as_float(__builtin_amdgcn_sbfe((int)es.mw, b0, 1) & __float_as_int(pa[2 * q]));
+            const float x1 = __int_as_float(__builtin_amdgcn_sbfe((int)es.mw, b1, 1) & __float_as_int(pa[2 * q + 1]));
+            es.hw[q] = s2_pk(x0, x1);
+        });
     };
     auto bfinish = [&](EpSt& es, S2Frag* O, auto rtc, u16* row0) {
         constexpr int rt = decltype(rtc)::value;
@@ -784,9 +815,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                             S2T_END(8);
                             S2T_BEGIN(13);
                             if constexpr (SPLITPK) fpackB(std::integral_constant<int, 15>());
-                            s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
-                                if (decltype(ec)::value >= MS * nk) fstep(prv, ec);
-                            });
+                            if constexpr (FIX && !SPLITPK) {  // (nk = NK0F: the count is compile-time)
+                                constexpr int E0 = MS * decltype(nk_tag)::value;
+                                if constexpr (E0 < 16) fsteps_free(prv, std::integral_constant<int, E0>());
+                            } else {
+                                s2_sfor<16>([&](auto ec) {  // steps not placed beside a live k-step
+                                    if (decltype(ec)::value >= MS * nk) fstep(prv, ec);
+                                });
+                            }
                             S2T_END(13);
                             S2T_BEGIN(10);
                             ffinish(l, std::integral_constant<int, rt - 1>(), save, srow, mks, false);
@@ -795,7 +831,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         if (rt == nrt - 1) {
                             S2T_BEGIN(13);
                             ep.bits = 0;
-                            s2_sfor<16>([&](auto ec) { fstep(cur, ec); });
+                            if constexpr (FIX) fsteps_free(cur, std::integral_constant<int, 0>());
+                            else s2_sfor<16>([&](auto ec) { fstep(cur, ec); });
                             ffinish(l, rtc, save, srow, mks, true);
                             S2T_END(13);
                         }
@@ -975,19 +1012,25 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                             gemm(cur, slot, &gB[s], &gB[s], 1, MBt(), NK1t(), nohook, PcOff());
                         } else {
                             eb.mw = mks_b(sp)[(lmask * C::NMW + (rp >> 1)) * 64 + lane];
-                            gemm(cur, slot + rt * 1024, &gB[s], &gB[s], 1, MBt(), NK1t(), [&](auto, auto pc) {
-                                s2_sfor<8>([&](auto ec) {
-                                    bstep(eb, prv, std::integral_constant<int, 8 * decltype(pc)::value + decltype(ec)::value>(),
-                                          std::integral_constant<int, rp>());
-                                });
-                            }, PcOff());
+                            if constexpr (FIX) {  // (2 MFMAs: no gaps worth filling)
+                                gemm(cur, slot + rt * 1024, &gB[s], &gB[s], 1, MBt(), NK1t(), nohook, PcOff());
+                                bsteps_free(eb, prv, std::integral_constant<int, rp>());
+                            } else {
+                                gemm(cur, slot + rt * 1024, &gB[s], &gB[s], 1, MBt(), NK1t(), [&](auto, auto pc) {
+                                    s2_sfor<8>([&](auto ec) {
+                                        bstep(eb, prv, std::integral_constant<int, 8 * decltype(pc)::value + decltype(ec)::value>(),
+                                              std::integral_constant<int, rp>());
+                                    });
+                                }, PcOff());
+                            }
                             S2T_BEGIN(11);
                             bfinish(eb, Do[sp], std::integral_constant<int, rp>(), brow[sp]);
                             S2T_END(11);
                         }
                         if (s == NS - 1 && rt == nrt - 1) {
                             eb.mw = mks_b(s)[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
-                            s2_sfor<16>([&](auto ec) { bstep(eb, cur, ec, rtc); });
+                            if constexpr (FIX) bsteps_free(eb, cur, rtc);
+                            else s2_sfor<16>([&](auto ec) { bstep(eb, cur, ec, rtc); });
                             bfinish(eb, Do[s], rtc, brow[s]);
                         }
                     });
@@ -1037,7 +1080,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         }
                         if (s == NS - 1 && rt == nrt - 1) {
                             eb.mw = mks_b(s)[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
-                            s2_sfor<16>([&](auto ec) { bstep(eb, cur, ec, rtc); });
+                            if constexpr (FIX) bsteps_free(eb, cur, rtc);
+                            else s2_sfor<16>([&](auto ec) { bstep(eb, cur, ec, rtc); });
                             bfinish(eb, Do[s], rtc, brow[s]);
                         }
                     });
