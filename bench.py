@@ -192,6 +192,23 @@ def prologue_rate(graph, var, L, c2f, n=20):
             "achieved": nbytes / s / 1e9, "unit": "GB/s", "peak": PEAK_HBM / 1e9, "frac": nbytes / s / PEAK_HBM}
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(n):
+    """Run this script on n ranks: python -m torch.distributed.run --nnodes=1 --nproc-per-node n
+    --master-addr 127.0.0.1 (the driver's own launch line) as a child process; its exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MARF_BENCH_LAUNCHER="bench.py --gpus (torch.distributed.run child)")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -207,24 +224,46 @@ def main():
     ap.add_argument("--cpu-sample-patches", type=int, default=4)
     ap.add_argument("--no-render", action="store_true",
                     help="skip the forward-only render rate (PMC passes: its launches share the step kernel's name)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="set up the ranks and print the JSON line's world size / backend only (no GPU work)")
     args = ap.parse_args()
     if args.precision is None:  # split-bf16 keeps 256-wide activations in registers: c5 runs plain bf16
         args.precision = "bf16" if max(CONFIGS[args.config][4]) > 256 else "bf16x3"
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` outside a launcher: start the N ranks (one process per GPU) through
+        # torch.distributed.run as a child, before anything here touches the GPU, and exit with its code
+        sys.exit(_self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks (WORLD_SIZE)")
     # rehearsal knobs for a one-GPU box (never set by the driver): every rank on cuda:0, gloo
     if os.environ.get("MARF_BENCH_ONE_DEVICE") == "1":
         local = 0
     backend = os.environ.get("MARF_BENCH_BACKEND", "nccl")  # "nccl" is RCCL on ROCm
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if args.launch_check:
+        dev = None
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
     if world > 1:
         if backend == "nccl":
             torch.distributed.init_process_group("nccl", device_id=dev)
         else:
             torch.distributed.init_process_group(backend)
+        world = torch.distributed.get_world_size()  # what the process group reports, not the env
+    dist = {"world_size": world, "backend": torch.distributed.get_backend() if world > 1 else None,
+            "launcher": os.environ.get("MARF_BENCH_LAUNCHER", "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ
+                                       else ("env" if "WORLD_SIZE" in os.environ else "single process"))}
+    if args.launch_check:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "n_gpus": world, "dist": dist, "launch_check": True}), flush=True)
+        if world > 1:
+            torch.distributed.barrier()
+            torch.distributed.destroy_process_group()
+        return
 
     import marf_hip
     from model import planar
@@ -378,6 +417,7 @@ def main():
                    "render_pixels_per_s": render_pps},
         "roofline": roof,
         "prologue": prologue,
+        "dist": dist,
         "kernels": per_kernel,
         "kernel_ms_per_step": step_kernel_ms,
     }

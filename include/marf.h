@@ -188,7 +188,10 @@ int marf_step_backward_ev(const marf_net* net, const marf_geometry* geo, const v
  * `nranks` on `device`.  marf_allreduce_grads sums a flat fp32 gradient in place on `stream`;
  * marf_allreduce_grads_layers sums each layer's span (marf_net_layer_span) on the communicator's
  * own stream after its marf_step_backward_ev event, so the exchange overlaps the remaining weight
- * gradients, and makes `stream` wait for the last one. */
+ * gradients, and makes `stream` wait for the last one.  A NULL entry of layer_events waits for the
+ * work queued on `stream` before the call.  marf_comm_create leaves the calling thread's current
+ * device unchanged.  After an error from either all-reduce call the ranks' collective sequences may
+ * disagree: destroy the communicator (every rank) rather than reuse it. */
 typedef struct marf_comm marf_comm;
 int marf_comm_unique_id(void* out, size_t cap);
 int marf_comm_create(const void* unique_id, int nranks, int rank, int device, marf_comm** out);

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "lib", "libmarf.so")
 # diagnostic variant with in-kernel phase stamps (tools/phase_stamps.py); never loaded by default
 LIB_STAMPS = os.path.join(HERE, "lib", "libmarf_stamps.so")
-SOURCES = ["marf_lie.hip", "marf_mlp.hip", "marf_wgrad.hip", "marf_step.hip", "marf_step2.hip", "marf_step3.hip", "marf_misc.hip", "marf_edge.hip", "marf_abi.hip", "marf_prof.hip", "marf_comm.hip"]
+SOURCES = ["marf_lie.hip", "marf_mlp.hip", "marf_wgrad.hip", "marf_step.hip", "marf_step2.hip", "marf_misc.hip", "marf_edge.hip", "marf_abi.hip", "marf_prof.hip", "marf_comm.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          # exact fp32 operation order for the bit-exact prologue (no implicit FMA contraction)
          "-ffp-contract=off", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function"]

@@ -46,7 +46,7 @@ static inline long long rup(long long x, long long m) { return (x + m - 1) / m *
 // step2 plan (the pixel-per-wave fused step, marf_step2.hip), filled by plan_step2_net
 struct Step2NetPlan {
     int variant;           // -1: not available for this net; 0: bf16 (8 waves); 1: split bf16 (4 waves);
-                           // 3: split bf16, two waves per SIMD (marf_step3.hip)
+                           // 2: bf16 on 4 waves (diagnostic)
     int NW, NS, HM, MAXR, NMW, slot, nk0, nta, n_stages, nbias, Kl, ldf0;
     int PX, TPX;           // pixels per wave, pixel slots per block tile
     int nslot;             // weight-ring slots in LDS
@@ -98,71 +98,14 @@ static bool step2_env_enabled() {
     return e && e[0] == '1';
 }
 
-int marf_step3_wave_lds_bytes();
 static int device_cus();
-
-// variant 3 (marf_step3.hip): k_step2's arithmetic on 16 pixels per wave (16x16x32 MFMAs, 8 waves,
-// 128-pixel block tiles as k_step2), 32 KB stages of 16-row tiles -- layer 0: r0 row tiles of nk0
-// operand pairs (k_step2's ng = ceil(L / 4) band chunks + the raw chunk, two per pair); hidden /
-// adjoint: two row tiles of 8 pairs; the last-layer dgrad: every row tile.  The adjoint has ng band
-// tiles + the raw tile.  Loss, dH and dW_last partials are k_step2's: one per 32-pixel set (PX).
-static void plan_step3_net(marf_net* n) {
-    Step2NetPlan& q = n->s2;
-    const int nl = n->n_layers;
-    q.variant = 3;
-    q.HM = 256;
-    q.NS = 1;
-    q.PX = 32;
-    q.NW = 8;
-    q.TPX = 128;
-    q.nslot = 3;
-    q.MAXR = 4;
-    q.NMW = 4;
-    q.slot = 32768;
-    const int ng = (n->L + 3) / 4;
-    q.nk0 = (ng + 2) / 2;
-    q.nta = ng + 1;
-    q.nk0w = ng + 1;
-    q.ldf0 = (int)rup(16 * q.nk0w, 32);
-    q.Kl = n->Kp[nl - 1];
-    int bo = 0;
-    for (int l = 0; l < nl; ++l) {
-        q.nrt[l] = l == nl - 1 ? 1 : n->Mp[l] / 16;
-        q.nrtb[l] = l == 0 ? q.nta : n->Kp[l] / 16;
-        q.boff[l] = bo;
-        bo += l == nl - 1 ? 32 : n->Mp[l];
-    }
-    q.nbias = bo;
-    q.r0 = std::max(2, (16 / q.nk0) & ~1);
-    q.ns0 = (q.nrt[0] + q.r0 - 1) / q.r0;
-    int st = q.ns0;
-    for (int l = 1; l < nl - 1; ++l) st += q.nrt[l] / 2;
-    q.n_fwd = st + 1;
-    st += 2;
-    for (int l = nl - 2; l >= 1; --l) st += q.nrtb[l] / 2;
-    st += (q.nta + 1) / 2;
-    q.n_stages = st;
-    q.prog_off = rup((long long)n->packed_bytes, 4096);
-    q.bias_off = q.prog_off + (size_t)st * q.slot;
-    q.kmap_off = rup((long long)(q.bias_off + (size_t)q.nbias * 4), 256);
-    q.end_off = rup((long long)(q.kmap_off + (size_t)n->D * 4), 256);
-}
 
 // Which pixel-per-wave variant (marf_step2.hip) runs this net, its weight-program shape and the
 // byte layout of the program / bias table / layer-0 column map appended to the packed buffer.
-// The split recipe has two kernels of identical arithmetic (k_step3 = k_step2 bit for bit). k_step2's
-// compile-time instantiations (full-width nets at L = 8, 9..12, 15, 16) are the faster ones at every
-// size measured (C3-shaped batches of 4..64 patches 10-12 %, C1 6 %: profiles/r4s); otherwise
-// k_step3 (two waves per SIMD) wins below about 48 block tiles of 128 pixels per CU (C1: 6.6 tiles,
-// -10 % against the generic k_step2) and loses above (C3: +4 %).  pixels_hint (the step's pixels per
-// GPU, 0 = unknown) picks; MARF_STEP3=0 / 1 at net creation forces one.
-static bool step2_specialized(const marf_net* n) {
-    const int nl = n->n_layers, L = n->L;
-    for (int l = 0; l < nl - 1; ++l)
-        if (n->Mp[l] != 256) return false;
-    const int nk0 = (L + 3) / 4 + 1, nta = (2 * L + 1 + 15) / 16;
-    return n->Kp[nl - 1] == 256 && ((nk0 == 5 && nta == 3) || (nk0 == 4 && nta == 2) || (nk0 == 3 && nta == 2));
-}
+// Full-width nets (every hidden layer 256 wide) at L = 8, 9..12, 13..15 and 16 run k_step2's
+// compile-time instantiations, every other net the generic k_step2 (the same arithmetic, so the same
+// bits: test_step2_bits_unchanged).  (Round 4's k_step3, the same bits at two waves per SIMD, was
+// slower than these instantiations at every size measured but 2 patches, profiles/r4s, and is gone.)
 static void plan_step2_net(marf_net* n, long long pixels_hint) {
     Step2NetPlan& q = n->s2;
     memset(&q, 0, sizeof(q));
@@ -176,16 +119,7 @@ static void plan_step2_net(marf_net* n, long long pixels_hint) {
     if (n->dtype != MARF_BF16X3 && !step2_env_enabled()) return;
     q.HM = 256;
     q.variant = n->dtype == MARF_BF16X3 ? 1 : 0;
-    if (q.variant == 1) {
-        const char* e = getenv("MARF_STEP3");
-        const bool step3 = (e && e[0]) ? e[0] == '1'
-                                       : !step2_specialized(n) && pixels_hint > 0 &&
-                                             pixels_hint < 48LL * 128 * device_cus();
-        if (step3) {
-            plan_step3_net(n);
-            return;
-        }
-    }
+    (void)pixels_hint;  // (kernel choice by size: none left to make)
     {
         const char* e = getenv("MARF_STEP2_NW4");  // diagnostic: plain bf16 on 4 waves per block
         if (q.variant == 0 && e && e[0] == '1') q.variant = 2;
@@ -544,7 +478,6 @@ int marf_net_layer_span(const marf_net* net, int l, long long* off, long long* l
 }
 const char* marf_net_step_kernel(const marf_net* net) {
     if (!net) return "";
-    if (net->s2.variant == 3) return "k_step3";
     if (net->s2.variant >= 0) return "k_step2";
     return "k_mlp_step";
 }
@@ -597,14 +530,9 @@ int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, vo
         }
         b.nbias = q.nbias;
         char* pk = (char*)d_packed;
-        if (q.variant == 3)
-            HIPCHK(marf_launch_pack3(d_params, pk + q.prog_off, (float*)(pk + q.bias_off), (int*)(pk + q.kmap_off), b,
-                                     (hipStream_t)stream),
-                   "net_pack step3");
-        else
-            HIPCHK(marf_launch_pack2(d_params, pk + q.prog_off, (float*)(pk + q.bias_off), (int*)(pk + q.kmap_off), b,
-                                     (hipStream_t)stream),
-                   "net_pack step2");
+        HIPCHK(marf_launch_pack2(d_params, pk + q.prog_off, (float*)(pk + q.bias_off), (int*)(pk + q.kmap_off), b,
+                                 (hipStream_t)stream),
+               "net_pack step2");
     }
     return MARF_OK;
 }
@@ -877,7 +805,7 @@ struct PipePlan {
 
 struct Step2BufPlan {
     size_t feat[MARF_MAX_LAYERS], dz[MARF_MAX_LAYERS];
-    size_t dH, loss, blast, wlast, dummy, xbuf, c2f, kmap, part, bpart, total;
+    size_t dH, loss, blast, wlast, dummy, c2f, kmap, part, bpart, total;
     size_t partl[MARF_MAX_LAYERS], bpartl[MARF_MAX_LAYERS];  // pipelined: per-layer split-K partials
     int grid, n_tiles;
     int nblk;  // per-block partial sets of the step kernel (all pieces' blocks)
@@ -910,7 +838,7 @@ static long long wgrad_chunk(long long S) {
 static bool l0_recompute(const marf_net* n, const GeoDev& g, long long S) {
     const char* e = getenv("MARF_F0_RECOMPUTE");
     if (e && e[0] == '0') return false;
-    if ((n->s2.variant != 1 && n->s2.variant != 3) || g.mode != MARF_GEO_GRID) return false;
+    if (n->s2.variant != 1 || g.mode != MARF_GEO_GRID) return false;
     const long long chunk = wgrad_chunk(S);
     return marf_wgrad_l0_recompute_ok(n->Mp[0], n->Kp[1], n->s2.ldf0, S, (int)chunk, (int)((S + chunk - 1) / chunk),
                                       g.Np_pad);
@@ -1031,9 +959,6 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
     off += rup((long long)p.nblk * 3 * q.Kl * 4, 256);
     p.dummy = off;
     off += rup((long long)p.grid * q.NW * 4096, 256);  // 64 B per lane
-    // k_step3: the dW_last partials a first-half wave hands to its second-half partner (12 x 16 B per lane)
-    p.xbuf = off;
-    if (q.variant == 3) off += rup((long long)p.grid * 4 * 12 * 32 * 16, 256);
     p.c2f = off;
     off += 256;
     p.kmap = off;  // the layer-0 column map, copied from the packed buffer by the forward
@@ -1099,16 +1024,12 @@ static int wgrad_piece(const marf_net* net, const GeoDev& g, const Step2BufPlan&
 
 static hipError_t launch_s2(const marf_net* n, const Step2Args& a, int grid, hipStream_t s) {
     const Step2NetPlan& q = n->s2;
-    if (q.variant != 3) {
-        // the compile-time layer-0 instantiations: split recipe, every hidden layer 256 wide, the
-        // layer-0 row tiles per stage the kernel derives from nk0, a 256-wide last-layer input
-        bool full = q.variant == 1 && q.nk0 >= 1 && q.r0 == std::max(1, std::min(8, 16 / q.nk0)) && q.Kl == 256;
-        for (int l = 0; l < n->n_layers - 1; ++l) full = full && n->Mp[l] == 256;
-        return marf_launch_step2(a, q.variant, grid, s, full ? q.nk0 : 0);
-    }
-    bool full = n->L >= 1;  // every hidden layer 256 wide
+    // the compile-time layer-0 instantiations: split recipe, every hidden layer 256 wide, the
+    // layer-0 row tiles per stage the kernel derives from nk0, a 256-wide last-layer input
+    bool full = q.variant == 1 && q.nk0 >= 1 && q.r0 == std::max(1, std::min(8, 16 / q.nk0)) && q.Kl == 256;
     for (int l = 0; l < n->n_layers - 1; ++l) full = full && n->Mp[l] == 256;
-    return marf_launch_step3(a, full, q.NW, grid, s);
+    if (const char* e = getenv("MARF_STEP2_GENERIC")) full = full && e[0] != '1';  // (A/B: the generic kernel)
+    return marf_launch_step2(a, q.variant, grid, s, full ? q.nk0 : 0);
 }
 
 static int step2_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
@@ -1164,7 +1085,6 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     a.Kl = q.Kl;
     a.c2f_w = (const float*)(sv + p.c2f);
     a.dummy = (float*)(sv + p.dummy);
-    a.xbuf = (float*)(sv + p.xbuf);
     a.stamps = g_stamps;
     a.n_tiles = p.n_tiles;
     // LDS layout
@@ -1180,8 +1100,7 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     off += (int)sizeof(S2Layer) * MARF_MAX_LAYERS;
     a.lds_wave = off;
     // per wave: transpose + g^T scratch, ReLU mask words of each pixel set of a dgrad pass, dW_last
-    a.lds_wave_bytes = q.variant == 3 ? marf_step3_wave_lds_bytes()
-                                      : (int)rup(2048 + q.NS * q.MAXR * q.NMW * 256 + 12 * q.Kl, 16);
+    a.lds_wave_bytes = (int)rup(2048 + q.NS * q.MAXR * q.NMW * 256 + 12 * q.Kl, 16);
     off += q.NW * a.lds_wave_bytes;
     a.lds_total = off;
     if (off > 160 * 1024) return fail(MARF_ERR_UNSUPPORTED, "step2: LDS plan %d B exceeds 160 KB", off);

@@ -105,7 +105,6 @@ struct Step2Args {
     int Kl;                          // padded input width of the last layer
     const float* c2f_w;              // [L] band weights of this step
     float* dummy;                    // [grid][NW][ST][64][2] store sink
-    float* xbuf;                     // k_step3: [grid][4][12][32][4] dW_last partials handed between waves
     unsigned long long* stamps;      // diagnostic builds (MARF_STAMPS): [grid][8] cycle totals of wave 0
     int tile0, n_tiles;              // this launch's block tiles [tile0, n_tiles) of 32 * NW pixel slots
     int fwd_only;                    // render: forward stages only, rgb out, nothing saved
@@ -166,10 +165,6 @@ hipError_t marf_launch_mlp_step(const marf::StepArgs& a, int dtype, int TP, int 
 hipError_t marf_launch_c2f_weights(const marf::C2fDev& c, int L, float* out, hipStream_t s);
 hipError_t marf_launch_loss_final(const double* part, int n, float* out, const float* denom_override, hipStream_t s);
 hipError_t marf_launch_step2(const marf::Step2Args& a, int variant, int grid, hipStream_t s, int full_nk0);
-hipError_t marf_launch_step3(const marf::Step2Args& a, bool full, int nw, int grid, hipStream_t s);
-bool marf_step3_nw_ok(bool full, int nk0, int nw);
-hipError_t marf_launch_pack3(const float* params, void* prog, float* bias_out, int* kmap, const marf::Pack2Args& a,
-                             hipStream_t s);
 hipError_t marf_launch_pack2(const float* params, void* prog, float* bias_out, int* kmap, const marf::Pack2Args& a,
                              hipStream_t s);
 hipError_t marf_launch_edge_map(const float* in, double* out, int n_img, int H, int W, hipStream_t s);

@@ -55,6 +55,7 @@ struct marf_comm {
     int device = 0, nranks = 1, rank = 0;
     hipStream_t side = nullptr;      // the per-layer exchanges
     hipEvent_t joined = nullptr;     // the last of them, for the caller's stream to wait on
+    hipEvent_t entry = nullptr;      // the caller's stream at the call (stands in for a NULL layer event)
 };
 
 // (marf_abi.hip's error slot)
@@ -82,6 +83,14 @@ int marf_comm_create(const void* unique_id, int nranks, int rank, int device, ma
     if (!unique_id || !out || nranks < 1 || rank < 0 || rank >= nranks)
         return marf_set_error(MARF_ERR_INVALID, "comm_create: bad arguments");
     if (!rccl().ok) return marf_set_error(MARF_ERR_UNSUPPORTED, "comm_create: librccl.so not found");
+    // the communicator is created on `device`; the calling thread's current device is restored on
+    // every path (no hidden global side effect)
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) return marf_set_error(MARF_ERR_HIP, "comm_create: hipGetDevice");
+    struct Restore {
+        int d;
+        ~Restore() { (void)hipSetDevice(d); }
+    } restore{prev};
     if (hipSetDevice(device) != hipSuccess) return marf_set_error(MARF_ERR_HIP, "comm_create: hipSetDevice");
     marf_comm* c = new marf_comm;
     c->device = device;
@@ -95,8 +104,11 @@ int marf_comm_create(const void* unique_id, int nranks, int rank, int device, ma
         return rccl_fail("ncclCommInitRank", r);
     }
     if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->joined, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->joined, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->entry, hipEventDisableTiming) != hipSuccess) {
         rccl().comm_destroy(c->comm);
+        if (c->joined) (void)hipEventDestroy(c->joined);
+        if (c->side) (void)hipStreamDestroy(c->side);
         delete c;
         return marf_set_error(MARF_ERR_HIP, "comm_create: stream / event");
     }
@@ -109,6 +121,7 @@ void marf_comm_destroy(marf_comm* c) {
     if (c->side) (void)hipStreamSynchronize(c->side);
     if (c->comm) rccl().comm_destroy(c->comm);
     if (c->joined) (void)hipEventDestroy(c->joined);
+    if (c->entry) (void)hipEventDestroy(c->entry);
     if (c->side) (void)hipStreamDestroy(c->side);
     delete c;
 }
@@ -120,24 +133,47 @@ int marf_allreduce_grads(marf_comm* c, float* d_flat, size_t n, void* stream) {
     return r == ncclSuccess ? MARF_OK : rccl_fail("ncclAllReduce", r);
 }
 
+// A NULL entry of layer_events (a layer the backward did not mark) waits for everything queued on
+// the caller's stream before this call instead.  If a collective fails after others were queued,
+// the caller's stream is still joined to the side stream before the error returns, but the ranks'
+// collective sequences may now disagree: destroy the communicator after an error (include/marf.h).
 int marf_allreduce_grads_layers(marf_comm* c, const marf_net* net, float* d_dparams, void* const* layer_events,
                                 void* stream) {
     if (!c || !net || !d_dparams || !layer_events) return marf_set_error(MARF_ERR_INVALID, "allreduce_grads_layers: NULL");
     const int nl = marf_net_layer_count(net);
     hipStream_t s = (hipStream_t)stream;
+    bool entry_recorded = false;
+    int rc = MARF_OK, queued = 0;
     // the order marf_step_backward_ev finishes them: last layer first
-    for (int l = nl - 1; l >= 0; --l) {
+    for (int l = nl - 1; l >= 0 && rc == MARF_OK; --l) {
         long long off = 0, len = 0;
-        if (marf_net_layer_span(net, l, &off, &len) != MARF_OK) return MARF_ERR_INVALID;
-        if (hipStreamWaitEvent(c->side, (hipEvent_t)layer_events[l], 0) != hipSuccess)
-            return marf_set_error(MARF_ERR_HIP, "allreduce_grads_layers: wait");
+        if (marf_net_layer_span(net, l, &off, &len) != MARF_OK) {
+            rc = MARF_ERR_INVALID;
+            break;
+        }
+        hipEvent_t ev = (hipEvent_t)layer_events[l];
+        if (!ev) {
+            if (!entry_recorded && hipEventRecord(c->entry, s) != hipSuccess) {
+                rc = marf_set_error(MARF_ERR_HIP, "allreduce_grads_layers: record");
+                break;
+            }
+            entry_recorded = true;
+            ev = c->entry;
+        }
+        if (hipStreamWaitEvent(c->side, ev, 0) != hipSuccess) {
+            rc = marf_set_error(MARF_ERR_HIP, "allreduce_grads_layers: wait");
+            break;
+        }
         ncclResult_t r = rccl().all_reduce(d_dparams + off, d_dparams + off, (size_t)len, ncclFloat32, ncclSum, c->comm,
                                            c->side);
-        if (r != ncclSuccess) return rccl_fail("ncclAllReduce (layer)", r);
+        if (r != ncclSuccess) rc = rccl_fail("ncclAllReduce (layer)", r);
+        else ++queued;
     }
+    if (rc != MARF_OK && queued == 0) return rc;  // nothing queued: the caller's stream is untouched
+    // join (also after a failure, so that the caller's stream never runs ahead of queued collectives)
     if (hipEventRecord(c->joined, c->side) != hipSuccess || hipStreamWaitEvent(s, c->joined, 0) != hipSuccess)
-        return marf_set_error(MARF_ERR_HIP, "allreduce_grads_layers: join");
-    return MARF_OK;
+        return rc != MARF_OK ? rc : marf_set_error(MARF_ERR_HIP, "allreduce_grads_layers: join");
+    return rc;
 }
 
 }  // extern "C"

@@ -1404,12 +1404,13 @@ static hipError_t launch_step2_t(const Step2Args& a, int grid, hipStream_t s) {
 // 256-wide, 4 waves (diagnostic: the variant-0 arithmetic at one wave per SIMD)
 // full_nk0: a full-width net's layer-0 k-step count (its r0 and row-tile counts follow from it; see
 // k_step2's NK0F), or 0 for the generic instantiation; the compile-time instantiations cover
-// (nk0, nta) = (5, 3): L = 15, 16; (4, 2): L = 9..12; (3, 2): L = 8
+// (nk0, nta) = (5, 3): L = 16; (5, 2): L = 13..15; (4, 2): L = 9..12; (3, 2): L = 8
 hipError_t marf_launch_step2(const Step2Args& a, int variant, int grid, hipStream_t s, int full_nk0) {
     switch (variant) {
         case 0: return launch_step2_t<256, false, 8, 4>(a, grid, s);
         case 1:
             if (full_nk0 == 5 && a.nta == 3) return launch_step2_t<256, true, 4, 4, 5, 3>(a, grid, s);
+            if (full_nk0 == 5 && a.nta == 2) return launch_step2_t<256, true, 4, 4, 5, 2>(a, grid, s);
             if (full_nk0 == 4 && a.nta == 2) return launch_step2_t<256, true, 4, 4, 4, 2>(a, grid, s);
             if (full_nk0 == 3 && a.nta == 2) return launch_step2_t<256, true, 4, 4, 3, 2>(a, grid, s);
             return launch_step2_t<256, true, 4, 4>(a, grid, s);

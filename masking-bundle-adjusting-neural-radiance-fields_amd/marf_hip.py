@@ -627,6 +627,7 @@ class _PlanarStepFunction(torch.autograd.Function):
         Bl = ctx.b1 - ctx.b0
         geo = engine.grid_geo(Bl, ctx.Hm)
         alloc = torch.empty if d_loss is not None else torch.zeros  # the step backward writes every element
+        engine.events_for = None  # set below only when this backward records the per-layer events
         dflat = alloc(engine.net.param_count, device=w.device, dtype=torch.float32)
         dh_local = alloc(Bl, 8, device=w.device, dtype=torch.float32)
         if d_loss is not None:

@@ -71,6 +71,7 @@ class Model(torch.nn.Module):
         self.lie = Lie()
         self.rank = torch.distributed.get_rank() if _dist() else 0
         self.world = torch.distributed.get_world_size() if _dist() else 1
+        self.exchange_counts = {"bucketed": 0, "flat": 0}  # which gradient exchange each step took
 
     # ------------------------------------------------------------------ data
     def load_dataset(self):
@@ -199,6 +200,9 @@ class Model(torch.nn.Module):
         flat = marf_hip.flat_view(grads)
         eng = self._grad_engine() if flat is not None and flat.is_cuda else None  # (gloo on CPU: flat)
         bucketed = eng is not None and eng.grad_events is not None and eng.events_for == flat.data_ptr()
+        if eng is not None:
+            eng.events_for = None  # the events mark this gradient only: never reused for a later one
+        self.exchange_counts["bucketed" if bucketed else "flat"] += 1
         if flat is not None and os.environ.get("MARF_GRAD_COMM") == "marf":
             if getattr(self, "_marf_comm", None) is None:
                 uid = [marf_hip.Comm.unique_id() if self.rank == 0 else None]

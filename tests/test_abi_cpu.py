@@ -72,33 +72,26 @@ def test_product_refuses_cpu_tensors(lib):
         marf_hip.sl3_to_SL3(torch.zeros(2, 8))
 
 
-def test_split_recipe_kernel_choice_by_size(lib, monkeypatch):
-    """marf_net_create_hint: the split recipe runs k_step2 wherever one of its compile-time
-    instantiations applies (full-width nets at L = 8, 9..12, 15, 16); otherwise k_step3 below 48
-    block tiles of 128 pixels per CU and k_step2 above (no GPU here: 256 CUs assumed, as on MI355X);
-    MARF_STEP3 forces either; the other recipes keep their kernels."""
+def test_split_recipe_kernel_choice(lib, monkeypatch):
+    """marf_net_create_hint: the split recipe runs k_step2 at every size (its compile-time
+    instantiations for full-width nets at L = 8, 9..12, 13..15, 16; the generic one otherwise), plain
+    bf16 / fp32 the tile kernel k_mlp_step unless MARF_STEP2=1."""
     import marf_hip
-    monkeypatch.delenv("MARF_STEP3", raising=False)
+    monkeypatch.delenv("MARF_STEP2", raising=False)
     c1 = 5 * 180 * 240
     c3 = 64 * 256 * 256
-    edge = 48 * 128 * 256
     full16 = [66, 256, 256, 256, 256, 3]
-    for L, dims in ((16, full16), (8, [34, 256, 256, 256, 256, 3]), (10, [42, 256, 256, 256, 256, 3])):
+    for L in (8, 10, 13, 15, 16):
+        dims = [2 + 4 * L, 256, 256, 256, 256, 3]
         for px in (c1, c3, 0):
             assert marf_hip.Net(dims, L, marf_hip.MARF_BF16X3, pixels_hint=px).step_kernel == "k_step2", (L, px)
-    narrow = [66, 128, 128, 3]  # generic instantiations: the size decides
-    assert marf_hip.Net(narrow, 16, marf_hip.MARF_BF16X3, pixels_hint=c1).step_kernel == "k_step3"
-    assert marf_hip.Net(narrow, 16, marf_hip.MARF_BF16X3, pixels_hint=edge - 1).step_kernel == "k_step3"
-    assert marf_hip.Net(narrow, 16, marf_hip.MARF_BF16X3, pixels_hint=edge).step_kernel == "k_step2"
-    assert marf_hip.Net(narrow, 16, marf_hip.MARF_BF16X3).step_kernel == "k_step2"  # size unknown
-    l13 = [54, 256, 256, 256, 256, 3]  # L = 13: nk0 5 but 2 adjoint tiles, no instantiation
-    assert marf_hip.Net(l13, 13, marf_hip.MARF_BF16X3, pixels_hint=c1).step_kernel == "k_step3"
-    monkeypatch.setenv("MARF_STEP3", "1")
-    assert marf_hip.Net(full16, 16, marf_hip.MARF_BF16X3, pixels_hint=c3).step_kernel == "k_step3"
-    monkeypatch.setenv("MARF_STEP3", "0")
-    assert marf_hip.Net(narrow, 16, marf_hip.MARF_BF16X3, pixels_hint=c1).step_kernel == "k_step2"
-    monkeypatch.delenv("MARF_STEP3")
+    for px in (c1, c3, 0):
+        assert marf_hip.Net([66, 128, 128, 3], 16, marf_hip.MARF_BF16X3, pixels_hint=px).step_kernel == "k_step2"
     assert marf_hip.Net(full16, 16, marf_hip.MARF_FP32, pixels_hint=c1).step_kernel == "k_mlp_step"
+    assert marf_hip.Net(full16, 16, marf_hip.MARF_BF16, pixels_hint=c3).step_kernel == "k_mlp_step"
+    monkeypatch.setenv("MARF_STEP2", "1")
+    assert marf_hip.Net(full16, 16, marf_hip.MARF_BF16, pixels_hint=c3).step_kernel == "k_step2"
+    monkeypatch.delenv("MARF_STEP2")
     spans = marf_hip.Net(full16, 16, marf_hip.MARF_BF16X3).layer_spans
     assert spans[0] == (0, 256 * 66 + 256) and sum(n for _, n in spans) == 215299
 
@@ -118,7 +111,7 @@ def test_bench_traffic_only_from_the_loaded_library(lib, tmp_path, monkeypatch):
     (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({"c3/bf16x3": entry}))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
     assert bench.pmc_traffic("c3", "bf16x3", "mlp_step", "k_step2")[0] == 3.0
-    assert bench.pmc_traffic("c3", "bf16x3", "mlp_step", "k_step3") is None     # another kernel
+    assert bench.pmc_traffic("c3", "bf16x3", "mlp_step", "k_mlp_step") is None  # another kernel
     assert bench.pmc_traffic("c3", "bf16", "mlp_step", "k_step2") is None       # no entry
     entry["source_hash"] = "0" * 40
     (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({"c3/bf16x3": entry}))

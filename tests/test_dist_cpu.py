@@ -79,3 +79,33 @@ def test_two_rank_sharding_and_allreduce(B):
     assert w0 == w1
     for b in range(B):
         assert w0[b] == [1.0 if b < B // 2 else 2.0] * 8
+
+
+def _bench(args, **env_over):
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                                "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env.update(MARF_BENCH_ONE_DEVICE="1", MARF_BENCH_BACKEND="gloo", **env_over)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    return r.returncode, lines, r.stderr
+
+
+def test_bench_gpus_flag_launches_the_ranks():
+    """`bench.py --gpus 2` outside a launcher starts two ranks itself (torch.distributed.run child,
+    before any GPU call) and the JSON line reports the world size the process group has and its
+    backend; a launcher whose WORLD_SIZE disagrees with --gpus is refused (bench.py main)."""
+    rc, lines, err = _bench(["--gpus", "2", "--launch-check"])
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1, lines  # rank 0 prints the one line
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["dist"]["world_size"] == 2 and d["dist"]["backend"] == "gloo", d
+    assert "torch.distributed.run" in d["dist"]["launcher"], d
+    rc, lines, err = _bench(["--gpus", "2", "--launch-check"], WORLD_SIZE="1")
+    assert rc != 0 and not lines and "WORLD_SIZE" in err
+    rc, lines, err = _bench(["--launch-check"])
+    assert rc == 0 and lines[0]["n_gpus"] == 1 and lines[0]["dist"]["world_size"] == 1, (rc, lines, err[-500:])

@@ -89,6 +89,7 @@ def _run(rank, world, port, precision, out, config="c1"):
         params = [p.detach().cpu().numpy().copy() for p in m.graph.neural_image.mlp.parameters()]
         if rank == 0:
             np.savez(out, losses=np.array(losses), warps=warps, shard=np.array(m.graph.shard or (0, opt.batch_size)),
+                     exchanges=np.array([m.exchange_counts["bucketed"], m.exchange_counts["flat"]]),
                      dh=dh, **{f"g{i}": a for i, a in enumerate(grads)}, **{f"p{i}": a for i, a in enumerate(params)},
                      **{f"i{i}": a for i, a in enumerate(init)})
     finally:
@@ -123,8 +124,11 @@ def test_bucketed_allreduce_equals_flat(tmp_path):
     2 ranks on the C1 batch, bf16x3, 3 full iterations."""
     a = _spawn(2, "bf16x3", str(tmp_path / "bucketed.npz"), "c1")
     b = _spawn(2, "bf16x3", str(tmp_path / "flat.npz"), "c1", env={"MARF_GRAD_BUCKETS": "0"})
+    # each run took the exchange it is meant to test (Model.exchange_counts: bucketed, flat)
+    assert a["exchanges"].tolist() == [STEPS, 0] and b["exchanges"].tolist() == [0, STEPS], (a["exchanges"], b["exchanges"])
     for k in a.files:
-        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+        if k != "exchanges":
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
 @pytest.mark.parametrize("precision,world,config", [("fp32", 2, "c1"), ("bf16x3", 2, "c1"), ("bf16x3", 4, "c1"),
@@ -217,4 +221,10 @@ def test_marf_comm_rccl_one_rank():
     comm.allreduce_layers(net, flat, ev)
     torch.cuda.synchronize()
     assert torch.equal(flat, ref)
+    ev.array[1] = None  # a layer without an event waits for the caller's stream instead
+    comm.allreduce_layers(net, flat, ev)
+    torch.cuda.synchronize()
+    assert torch.equal(flat, ref)
+    # the communicator's creation left this thread's current device alone
+    assert torch.cuda.current_device() == 0
     del comm

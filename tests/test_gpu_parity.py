@@ -815,12 +815,11 @@ def _reference_runs():
     return runs
 
 
-@pytest.mark.parametrize("precision", ["bf16x3", "bf16x3-step3", "fp32"])
-def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path, monkeypatch):
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path):
     """BASELINE config 1/2 end to end: the seed=3 cat_batch3 run for 3000 iterations, for the bench
-    recipe on the kernel the library picks (bf16x3: k_step2's compile-time L = 8 instantiation, the
-    kernel family bench.py times at C3) and on the other one (bf16x3-step3: k_step3) -- they compute
-    the same bits (test_step3_bitwise_equals_step2), so they end in the same state -- and for fp32.
+    recipe (bf16x3: k_step2's compile-time L = 8 instantiation, the kernel family bench.py times at
+    C3, whose bits test_step2_bits_unchanged pins) and for fp32.
 
     PSNR: final within 0.05 dB of the reference's 25.9968 dB (north_star).
     Warps: the north_star's 1e-2 cannot be met against a single reference run by the reference
@@ -832,10 +831,6 @@ def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path, monkeypatch):
     The run is chaotic: which basin patch 1's perspective row settles in (26.0 dB or 24.3-25.0 dB)
     is re-rolled by any change of fp32 rounding order, so the kernel the bench times must be the
     kernel whose arithmetic this run pins."""
-    monkeypatch.delenv("MARF_STEP3", raising=False)
-    if precision == "bf16x3-step3":
-        monkeypatch.setenv("MARF_STEP3", "1")
-        precision = "bf16x3"
     psnr, warps = _run_c1(precision, tmp_path)
     runs = _reference_runs()
     err = warps[1:] - REF_WARPS_3000
@@ -994,18 +989,14 @@ def test_canvas_geometry_fused_steps_vs_oracle(precision, tmp_path):
         m.graph.warp_param.weight.data[0] = 0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3-step2", "bf16x3-step3"])
-def test_c3_two_patch_step_vs_oracle(precision, tmp_path, monkeypatch):
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_c3_two_patch_step_vs_oracle(precision, tmp_path):
     """C3 shape (256x256 crops of a 512 canvas, L=16, 4x256), 2 patches, non-zero warps on both.
-    bf16x3 on each of the recipe's two step kernels (MARF_STEP3=0: k_step2, 1: k_step3).
     rgb <= 1e-5 abs and loss vs oracle.PlanarStep (fp32 <= 1e-6 rel).  Gradients against the
     float64 reference ops: fp32 within 1e-5 relative to their max OR within 2x the reference's own
     fp32 error, whichever is larger (_compare_step); bf16x3 (the bench recipe) within 1e-2 (north_star
     bf16 bound) AND within 2x the reference's own fp32 error (measured: MLP 4.9e-4 vs the
     reference's 4.7e-4; d warp 6.9e-3 vs 5.3e-3 -- a 2 x 65,536-pixel sum that cancels)."""
-    if precision.startswith("bf16x3-"):
-        monkeypatch.setenv("MARF_STEP3", "1" if precision.endswith("step3") else "0")
-        precision = "bf16x3"
     m, var, inputs = _synthetic_setup(precision, tmp_path, 2, 256, 16, [256] * 4)
     o = _compare_step(m, var, inputs, precision, 5)
     assert o["rgb"] <= 1e-5
@@ -1018,85 +1009,119 @@ def test_c3_two_patch_step_vs_oracle(precision, tmp_path, monkeypatch):
         assert o["grad_err"] <= 2 * o["grad_err_ref32"] and o["dh_err"] <= 2 * o["dh_err_ref32"], o
 
 
-_STEP3_CASES = {
-    # name: (B, crop, L, hidden); tile counts per block of the 256-block grid in brackets
-    "c1": None,                                   # cat_batch3, 5 x 180x240, L=8 (6 or 7)
-    "c3x2": (2, 256, 16, [256] * 4),              # C3 shape (4), odd layer-0 chunk count (5)
-    "c3x3-L10": (3, 256, 10, [256] * 4),          # even layer-0 chunk count (4) (6)
-    "L16-1tile": (2, 100, 16, [256] * 4),         # 158 tiles: one tile per block, 98 idle blocks
-    "narrow": (2, 64, 8, [128, 96, 128]),         # the generic instantiations (widths < 256)
-    "L13": (2, 128, 13, [256] * 4),               # full width, generic k_step2 (nk0 5, 2 adjoint tiles)
-}
-
-
-def _kernel_model(case, kernel, tmp_path, monkeypatch):
-    """The bf16x3 product model of a _STEP3_CASES case whose step runs `kernel` (MARF_STEP3 is read
-    when the engine's net is created)."""
-    import time
-    from util import EasyDict as edict
-    monkeypatch.setenv("MARF_STEP3", "1" if kernel == "k_step3" else "0")
-    inputs = None
-    if _STEP3_CASES[case] is None:
-        m, var = c1_setup("bf16x3", tmp_path / kernel)
-    else:
-        B, crop, L, hidden = _STEP3_CASES[case]
-        m, var, inputs = _synthetic_setup("bf16x3", tmp_path / kernel, B, crop, L, hidden)
-        m.timer = edict(start=time.time(), it_mean=None)
-    assert m.graph.neural_image.engine(torch.device(DEV)).net.step_kernel == kernel
-    monkeypatch.delenv("MARF_STEP3", raising=False)
-    return m, var, inputs
-
-
-@pytest.mark.parametrize("kernel", ["k_step2", "k_step3"])
-def test_bf16x3_odd_width_vs_oracle(kernel, tmp_path, monkeypatch):
-    """Hidden widths of 32 mod 64 (an odd number of 32-row tiles; here 96) on the split-bf16 step
-    kernels, against the oracle (rgb, loss) and the reference ops in float64 (gradients): the bf16x3
+def test_bf16x3_odd_width_vs_oracle(tmp_path):
+    """Hidden widths of 32 mod 64 (an odd number of 32-row tiles; here 96) on the generic split-bf16
+    k_step2, against the oracle (rgb, loss) and the reference ops in float64 (gradients): the bf16x3
     forward bound (rgb <= 1e-5) and the north_star bf16 bound on the gradients (<= 1e-2 of their max),
     with cosine >= 0.9999.  (k_step2 lost the ReLU mask word of such a layer's last row tile before
     round 4.)"""
-    m, var, inputs = _kernel_model("narrow", kernel, tmp_path, monkeypatch)
-    o = _compare_step(m, var, inputs, "bf16x3", len(_STEP3_CASES["narrow"][3]) + 1)
+    hidden = [128, 96, 128]
+    m, var, inputs = _synthetic_setup("bf16x3", tmp_path, 2, 64, 8, hidden)
+    assert m.graph.neural_image.engine(torch.device(DEV)).net.step_kernel == "k_step2"
+    o = _compare_step(m, var, inputs, "bf16x3", len(hidden) + 1)
     assert o["rgb"] <= 1e-5 and o["loss"] <= 1e-5, o
     assert o["grad_err"] <= 1e-2 and o["dh_err"] <= 1e-2, o
     assert o["grad_cos"] >= 0.9999 and o["dh_cos"] >= 0.9999, o
 
 
-@pytest.mark.parametrize("case", list(_STEP3_CASES))
-def test_step3_bitwise_equals_step2(case, tmp_path, monkeypatch):
-    """k_step3 (two waves per SIMD) computes k_step2's arithmetic: the first step's rgb, loss, every
-    MLP gradient and the warp gradient are bit-identical, and so are the parameters and warps after
-    two more full training iterations (Adam, progress, fix_first).  This is what lets the faster
-    kernel inherit k_step2's seed-3 run (test_c1_3000_iterations_psnr_and_warps)."""
-    res = {}
-    for kernel in ("k_step2", "k_step3"):
-        m, var, _ = _kernel_model(case, kernel, tmp_path, monkeypatch)
-        v, loss = one_step_grads(m, var)
-        r = {"rgb": v.rgb_prediction.detach().cpu(), "loss": loss.rgb.detach().cpu(),
-             "dh": m.graph.warp_param.weight.grad.detach().cpu()}
-        for i, lay in enumerate(m.graph.neural_image.mlp):
-            r[f"dW{i}"] = lay.weight.grad.detach().cpu()
-            r[f"db{i}"] = lay.bias.grad.detach().cpu()
-        m.optim.step()
-        m.graph.warp_param.weight.data[0] = 0
-        for _ in range(2):
-            r.setdefault("losses", []).append(float(m.train_iteration(var, _Loader()).rgb))
-            m.graph.warp_param.weight.data[0] = 0
-        r["warp"] = m.graph.warp_param.weight.detach().cpu()
-        for i, lay in enumerate(m.graph.neural_image.mlp):
-            r[f"W{i}"] = lay.weight.detach().cpu()
-        res[kernel] = r
-    a, b = res["k_step2"], res["k_step3"]
-    bad = []
-    for k in a:
-        if k == "losses":
-            if a[k] != b[k]:
-                bad.append((k, a[k], b[k]))
-        elif not torch.equal(a[k].view(torch.int32), b[k].view(torch.int32)):  # bits, signs of zeros included
-            d = (a[k].double() - b[k].double()).abs()
-            bad.append((k, int((d > 0).sum()), float(d.max())))
-    for x in bad:
-        print("differs:", x)
-    assert not bad, [x[0] for x in bad]
+def _bits_fixture():
+    import json
+    import step_bits
+    return json.load(open(step_bits.BITS_JSON))
+
+
+@pytest.mark.parametrize("case", ["c1", "c3x2", "c3x3-L10", "L16-1tile", "narrow", "L13", "L15", "c1-generic",
+                                  "c3x2-generic"])
+def test_step2_bits_unchanged(case, monkeypatch):
+    """The split-bf16 step computes the bits the seed-3 run was pinned on: rgb, loss, every MLP
+    gradient and d warp of one fused step, then the losses, warps and weights after two more
+    Model.train_iteration calls, hash for hash equal to tests/golden/step2_bits.json (written on an
+    MI355X by tools/make_step2_bits.py from the round-4 library, commit d3c2143).  Covers every
+    compile-time instantiation of k_step2 (L = 8, 9..12, 13..15, 16), the generic kernel (narrow
+    widths) and one tile per block; "-generic": the same case on the generic kernel
+    (MARF_STEP2_GENERIC=1), which must give the instantiation's bits.  (The 64-patch headline
+    case: test_c3_headline_step.)"""
+    import step_bits
+    if case.endswith("-generic"):
+        case = case[:-len("-generic")]
+        monkeypatch.setenv("MARF_STEP2_GENERIC", "1")
+    ref = _bits_fixture()["cases"][case]
+    got = step_bits.case_bits(case)
+    bad = sorted(k for k in ref["bits"] if got["bits"].get(k) != ref["bits"][k])
+    assert not bad, (case, got["kernel"], bad)
+
+
+def test_c3_headline_step():
+    """The benched step at the headline size (BASELINE C3: 64 patches x 256x256, L = 16, 66-256x4-3,
+    bf16x3 on k_step2<256, true, 4, 4, 5, 3>, 2,048 block tiles = 8 per persistent block) through
+    the product's Model (model/planar.py:187-209):
+      * bits: one fused step and two Model.train_iteration calls hash-equal to the round-4 library's
+        (tests/golden/step2_bits.json "c3x64"), and a rerun from the same state is bit-identical;
+      * linearity: d loss x 2 gives exactly 2 x every MLP gradient and d warp;
+      * rgb of 512 sampled pixels per patch (all 64 patches) within 1e-5 of the oracle's fp32
+        forward (oracle.mlp_forward on the oracle's grid / warp / posenc);
+      * d warp of two sampled patches (each patch's d warp depends only on its own pixels, scaled by
+        the global 3 sum(mask)) within 1e-2 of the float64 reference ops (cpu_ref) on those patches,
+        and within 2x the reference's own fp32 error there."""
+    import cpu_ref
+    import step_bits
+    m, var = step_bits.build_case("c3x64")
+    eng = m.graph.neural_image.engine(torch.device(DEV))
+    assert eng.net.step_kernel == "k_step2" and m.batch_size == 64
+    params = [(l.weight.detach().cpu().numpy().copy(), l.bias.detach().cpu().numpy().copy()) for l in m.graph.neural_image.mlp]
+    warp = m.graph.warp_param.weight.detach().cpu().numpy().copy()
+    rgb_t = m.images.rgb.cpu().numpy()
+    mask_t = m.images.masks.cpu().numpy()
+
+    def step(scale):
+        m.optim.zero_grad()
+        v = m.graph.forward(var, mode="train")
+        loss = m.summarize_loss(m.graph.compute_loss(v, mode="train"))
+        (loss.all * scale).backward()
+        return (v.rgb_prediction.detach().clone(), float(loss.rgb), m.graph.warp_param.weight.grad.detach().clone(),
+                [p.grad.detach().clone() for p in m.graph.neural_image.mlp.parameters()])
+
+    rgb1, l1, dh1, g1 = step(1.0)
+    rgb2, l2, dh2, g2 = step(1.0)
+    _, l3, dh3, g3 = step(2.0)
+    assert torch.equal(rgb1, rgb2) and l1 == l2 == l3 and torch.equal(dh1, dh2)
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+    assert torch.equal(2 * dh1, dh3) and all(torch.equal(2 * a, b) for a, b in zip(g1, g3))
+    assert all(torch.isfinite(a).all() for a in g1) and torch.isfinite(dh1).all()
+
+    # rgb: 512 seeded pixels of every patch against the oracle's forward
+    rng = np.random.default_rng(11)
+    idx = np.sort(rng.choice(256 * 256, 512, replace=False))
+    xy = oracle.pixel_grid(512, 512, 256, 256)[idx]
+    Hm = oracle.sl3_to_SL3(warp)  # all 64 at once: torch's batched matrix_exp path, as the library
+    uv = oracle.warp_points(np.ascontiguousarray(np.broadcast_to(xy, (64,) + xy.shape)), Hm)
+    f0 = oracle.posenc_features(uv, 16, oracle.c2f_weights(np.float32(0.2), [0, 0.4], 16)).reshape(-1, 66)
+    ref_rgb = oracle.mlp_forward(f0, params)[1].reshape(64, 512, 3)
+    err = float(np.abs(rgb1.cpu().numpy()[:, idx] - ref_rgb).max())
+    print(f"C3 headline: rgb max |err| over 64 x 512 pixels {err:.3g}")
+    assert err <= 1e-5, err
+
+    # d warp of two patches against the float64 reference ops on those patches alone
+    sel = [17, 50]
+    cfg = dict(H=512, W=512, patch_H=256, patch_W=256, L=16, c2f=[0, 0.4], max_iter=3000, lr=1e-3, lr_warp=1e-3,
+               fix_first=True, use_edges=False, alpha_initial=0.0, alpha_final=1.0)
+    scale = float(mask_t[sel].sum(dtype=np.float64) / mask_t.sum(dtype=np.float64))  # the denominators' ratio
+    truth = {}
+    for tag, dtype, dev in (("f64", torch.float64, DEV), ("ref32", torch.float32, "cpu")):
+        cpu_ref.set_threads()
+        s = cpu_ref.CpuRefStep(cfg, params, warp[sel], rgb_t[sel], mask_t[sel], dtype=dtype, device=dev)
+        s.progress.data.fill_(0.2)
+        truth[tag] = np.asarray(s.step()["dh"], np.float64) * scale
+    ours = dh1.cpu().numpy()[sel]
+    e_ours, e_ref = _err(ours, truth["f64"]), _err(truth["ref32"], truth["f64"])
+    print(f"C3 headline: d warp of patches {sel}: error {e_ours:.3g} (the reference's fp32: {e_ref:.3g})")
+    assert e_ours <= 1e-2 and e_ours <= 2 * e_ref, (e_ours, e_ref)
+
+    # the same state's bits, step and two training iterations, against the round-4 library's
+    got = step_bits.case_bits("c3x64")
+    ref = _bits_fixture()["cases"]["c3x64"]
+    bad = sorted(k for k in ref["bits"] if got["bits"].get(k) != ref["bits"][k])
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("c2f", [(0, 0.4), None], ids=["c2f", "noc2f"])

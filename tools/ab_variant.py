@@ -1,0 +1,58 @@
+"""Timing-only library variants, built from patched copies of csrc/ (the production sources stay
+free of diagnostic switches):  python tools/ab_variant.py NAME [NAME ...]  ->  lib/libmarf_ab_NAME.so
+
+  nodma          k_step2 without its weight-ring DMA pieces (the ring keeps whatever the slots
+                 held): what the step kernel costs without streaming its weight program
+  nosave         k_step2 without its saved-tensor stores (feat_l, dz_l) and their vmcnt accounting
+  nodma_nosave   both
+
+Their results are wrong on purpose: bench them with MARF_AB_TIMING_ONLY=1 and MARF_LIB=<the .so>
+(bench.py then never reports the line as a headline)."""
+import os
+import shutil
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "masking-bundle-adjusting-neural-radiance-fields_amd")
+sys.path.insert(0, PKG)
+
+DMA_ASM = ('asm volatile("s_mov_b32 %0, m0\\n\\ts_mov_b32 m0, %2\\n\\ts_nop 0\\n\\tglobal_load_lds_dwordx4 %1, off offset:%3\\n\\ts_mov_b32 m0, %0"\n'
+           '                     : "=&s"(keep)\n'
+           '                     : "v"(va), "s"(m), "n"((j & 3) * 1024)\n'
+           '                     : "memory");')
+SAVE = ("        s2_st16o<64 * rt>(row0, contig(f0));\n"
+        "        s2_st16o<64 * rt + 32>(row0, contig(f1));\n"
+        "        st_cur += 2;\n")
+
+PATCHES = {
+    "nodma": [("marf_step2.hip", DMA_ASM, "(void)va; (void)m; keep = 0; (void)keep;")],
+    "nosave": [("marf_step2.hip", SAVE, "        (void)row0; (void)f0; (void)f1; (void)contig;\n")],
+}
+PATCHES["nodma_nosave"] = PATCHES["nodma"] + PATCHES["nosave"]
+
+
+def build(name):
+    import build_lib
+    with tempfile.TemporaryDirectory() as td:
+        pkg = os.path.join(td, "pkg")
+        shutil.copytree(os.path.join(PKG, "csrc"), os.path.join(pkg, "csrc"))
+        shutil.copytree(os.path.join(ROOT, "include"), os.path.join(td, "include"))  # (csrc includes ../../include)
+        for fn, old, new in PATCHES[name]:
+            p = os.path.join(pkg, "csrc", fn)
+            src = open(p).read()
+            if src.count(old) != 1:
+                raise SystemExit(f"{name}: patch target not found exactly once in {fn}")
+            open(p, "w").write(src.replace(old, new))
+        # compile the patched copy with the production flags (build_lib reads csrc/ next to HERE)
+        here = build_lib.HERE
+        try:
+            build_lib.HERE = pkg
+            build_lib._compile(os.path.join(PKG, "lib", f"libmarf_ab_{name}.so"), [], True)
+        finally:
+            build_lib.HERE = here
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:]:
+        build(n)

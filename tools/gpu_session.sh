@@ -1,0 +1,71 @@
+#!/bin/bash
+# One GPU session, steps chosen on the command line (replaces the per-round gpu_r*.sh one-offs):
+#   bash tools/gpu_session.sh <tag> <step> [<step> ...]
+# steps:
+#   tests[=<pytest -k expr>]  the GPU suite (or a -k selection) -> <tag>/gpu_tests.log
+#   smoke                     __graft_entry__.smoke()
+#   bench                     the default bench line (C3 headline, CPU baseline) -> <tag>/bench.json
+#   prof                      rocprofv3 --kernel-trace --stats of a short C3 bench -> <tag>/prof/
+#   bits                      tools/make_step2_bits.py -> <tag>/step2_bits.json
+#   ab=<v1,v2,...>            C3 bench of lib/libmarf_<v>.so variants ("default" = lib/libmarf.so),
+#                             alternating twice (timing-only variants: MARF_AB_TIMING_ONLY=1)
+#   cfg                       secondary bench lines (tools/bench_configs.sh)
+#   pmc=<config>/<precision>  FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh)
+# Every GPU step has its own time limit; the session stops at the first failure, abort or timeout.
+set -o pipefail
+TAG=$1; shift
+OUT=$PWD/gpurun_out/$TAG
+ROOT=$PWD
+LIBD=$ROOT/masking-bundle-adjusting-neural-radiance-fields_amd/lib
+mkdir -p $OUT
+line() {  # summary of a bench json
+  python - "$1" "$2" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+k = d.get("kernels", {})
+r = d.get("roofline") or {}
+print("%-22s %.4g px/s  %.3f ms/step  %s %.3f ms  frac %s  kernels/step %.3f ms" % (
+    sys.argv[2], d["value"], d["ms_per_step"], r.get("kernel"), r.get("avg_launch_ms", 0), r.get("frac"),
+    d.get("kernel_ms_per_step", 0)) + "  " + " ".join("%s=%.3f" % (n, v["avg_ms"] * v["launches_per_step"]) for n, v in
+                                                      sorted(k.items(), key=lambda kv: -kv[1]["avg_ms"] * kv[1]["launches_per_step"])[:6]))
+PY
+}
+for step in "$@"; do
+  case $step in
+    tests|tests=*)
+      K=${step#tests}; K=${K#=}
+      if [ -n "$K" ]; then SEL=(-k "$K"); else SEL=(); fi
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread "${SEL[@]}" > $OUT/gpu_tests.log 2>&1
+      RC=$?; tail -3 $OUT/gpu_tests.log
+      [ $RC = 0 ] || { echo "pytest exit $RC: stopping"; exit $RC; } ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -5 $OUT/smoke.log; exit 1; }
+      tail -1 $OUT/smoke.log ;;
+    bench)
+      timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -5 $OUT/bench.err; exit 1; }
+      line $OUT/bench.json bench ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+         python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render > $OUT/prof.log 2>&1) || { echo "rocprof failed"; tail -5 $OUT/prof.log; exit 1; }
+      find $OUT/prof -name "*kernel_stats*" | head -3 ;;
+    bits)
+      timeout -k 10 300 python tools/make_step2_bits.py $OUT/step2_bits.json > $OUT/bits.log 2>&1 || { echo "bits failed"; tail -5 $OUT/bits.log; exit 1; }
+      tail -2 $OUT/bits.log ;;
+    ab=*)
+      IFS=, read -ra VS <<< "${step#ab=}"
+      for rep in 1 2; do
+        for v in "${VS[@]}"; do
+          if [ "$v" = default ]; then L=""; TO=""; else L=$LIBD/libmarf_$v.so; TO=$([[ $v == ab_* ]] && echo 1); fi
+          MARF_LIB=$L MARF_AB_TIMING_ONLY=$TO timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render \
+            > $OUT/ab_$v.json 2> $OUT/ab_$v.err || { echo "ab $v failed"; tail -5 $OUT/ab_$v.err; exit 1; }
+          line $OUT/ab_$v.json "$v"
+        done
+      done ;;
+    cfg)
+      bash tools/bench_configs.sh $TAG/cfg || exit 1 ;;
+    pmc=*)
+      C=${step#pmc=}
+      bash tools/pmc_traffic.sh $TAG/pmc_${C%/*} ${C%/*} ${C#*/} || exit 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
