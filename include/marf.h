@@ -111,13 +111,13 @@ int marf_prologue_probe(const marf_geometry* geo, const marf_c2f* c2f, int L, co
  * Flat fp32 parameter vector layout = NeuralImageFunction.mlp parameters in module order:
  * W0 [dims1][dims0], b0 [dims1], W1, b1, ...  (nn.Linear layout). */
 int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** out);
-/* As marf_net_create, with the pixels one fused step will process on this GPU (0 = unknown): it picks
- * the faster of the split recipe's two step kernels for that size (they compute the same bits). */
+/* As marf_net_create, with the pixels one fused step will process on this GPU (0 = unknown; kept for
+ * size-dependent kernel choices: the split recipe runs k_step2 at every size today). */
 int marf_net_create_hint(int n_layers, const int* dims, int L, int dtype, long long pixels_hint, marf_net** out);
 void marf_net_destroy(marf_net* net);
 long long marf_net_param_count(const marf_net* net);
 size_t marf_net_packed_bytes(const marf_net* net);
-/* Name of the kernel that runs this net's fused training step ("k_step2", "k_step3", "k_mlp_step"),
+/* Name of the kernel that runs this net's fused training step ("k_step2" or "k_mlp_step"),
  * fixed at net creation (no reference counterpart: measurement and test bookkeeping). */
 const char* marf_net_step_kernel(const marf_net* net);
 /* Layer l's parameters in the flat vector: W_l [dims[l+1]][dims[l]] then b_l, from *off, *len floats. */
@@ -228,6 +228,10 @@ int marf_adam_step(float* d_p, const float* d_g, float* d_m, float* d_v, long lo
  * marf_profile_read drains the recorded pairs (synchronising on them) and returns, per kernel
  * name, the summed duration (ms) and launch count; names is a [cap][name_len] char array. */
 int marf_profile_enable(int on);
+/* Restrict the timing to the kernels named in `names` (comma-separated profile names, e.g.
+ * "mlp_step"; NULL or "" = every kernel), so a timed region pays for the event pairs of the kernels
+ * it reports only (each pair adds a few microseconds between launches). */
+int marf_profile_filter(const char* names);
 int marf_profile_reset(void);
 int marf_profile_read(char* names, int name_len, double* total_ms, long long* count, int cap);
 

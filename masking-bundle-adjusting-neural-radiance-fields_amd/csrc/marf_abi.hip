@@ -806,7 +806,7 @@ struct PipePlan {
 struct Step2BufPlan {
     size_t feat[MARF_MAX_LAYERS], dz[MARF_MAX_LAYERS];
     size_t dH, loss, blast, wlast, dummy, c2f, kmap, part, bpart, total;
-    size_t partl[MARF_MAX_LAYERS], bpartl[MARF_MAX_LAYERS];  // pipelined: per-layer split-K partials
+    size_t partl[MARF_MAX_LAYERS], bpartl[MARF_MAX_LAYERS];  // per-layer split-K partials (pipelined / fused)
     int grid, n_tiles;
     int nblk;  // per-block partial sets of the step kernel (all pieces' blocks)
     long long S;
@@ -988,6 +988,15 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
         off += rup(Ssave * std::max(n_chunks * mxo, 256LL * (3 * q.Kl + 3)) * 4, 256);
         p.bpart = off;
         off += rup(Ssave * n_chunks * mxm * 4, 256);
+        // the fused weight gradients keep every layer's partials at once (layer 0: part)
+        p.partl[0] = p.part;
+        p.bpartl[0] = p.bpart;
+        for (int l = 1; l < nl - 1; ++l) {
+            p.partl[l] = off;
+            off += rup(Ssave * n_chunks * n->Mp[l] * n->Kp[l] * 4, 256);
+            p.bpartl[l] = off;
+            off += rup(Ssave * n_chunks * n->Mp[l] * 4, 256);
+        }
     }
     p.total = off;
 }
@@ -1170,6 +1179,66 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
     float* bpart = (float*)(sv + p.bpart);
     const float* denom = d_loss_out + 1;
     const int nl = net->n_layers;
+    // The fused weight gradients (marf_launch_wgrad_fused): the hidden layers in one launch, layer 0
+    // beside it on the side stream, every reduction in one launch -- the same partials and sums as
+    // the per-layer launches below (bit-identical).  The layer events follow it, in the per-layer order.
+    if (d_dparams && !p.pipe.on) {
+        const long long chunk = wgrad_chunk(p.S);
+        const int n_chunks = (int)((p.S + chunk - 1) / chunk);
+        const int* kmap = (const int*)(sv + p.kmap);
+        const bool f0 = l0_recompute(net, g, p.S);
+        WgFusedLayer Lf[MARF_MAX_LAYERS];
+        memset(Lf, 0, sizeof(Lf));
+        int nf = 0;
+        {
+            const int l = nl - 1;  // the last layer: the step kernel's per-block partials
+            WgFusedLayer& x = Lf[nf++];
+            x.kind = 3;
+            x.partial = (float*)(sv + p.wlast);
+            x.bpartial = (float*)(sv + p.blast);
+            x.n_parts = p.nblk;
+            x.M = 3;
+            x.K = q.Kl;
+            x.Mo = 3;
+            x.Ko = net->dims[l];
+            x.dW = d_dparams + net->w_off[l];
+            x.db = d_dparams + net->b_off[l];
+        }
+        for (int l = nl - 2; l >= 0; --l) {
+            WgFusedLayer& x = Lf[nf++];
+            x.kind = l > 0 ? 0 : (f0 ? 1 : 2);
+            x.dz = sv + p.dz[l + 1];
+            x.ldz = net->Kp[l + 1];
+            x.feat = (l == 0 && f0) ? nullptr : sv + p.feat[l];
+            x.ldf = x.K = l == 0 ? q.ldf0 : net->Kp[l];
+            x.M = net->Mp[l];
+            x.partial = (float*)(sv + p.partl[l]);
+            x.bpartial = (float*)(sv + p.bpartl[l]);
+            x.n_parts = n_chunks;
+            x.Mo = net->dims[l + 1];
+            x.Ko = net->dims[l];
+            x.dW = d_dparams + net->w_off[l];
+            x.db = d_dparams + net->b_off[l];
+            x.kmap = l == 0 ? kmap : nullptr;
+        }
+        if (marf_wgrad_fused_ok(Lf, nf, p.S, (int)chunk, n_chunks, g.Np_pad)) {
+            PipeStreams* st = nullptr;
+            rc = pipe_streams(&st);
+            if (rc) return rc;
+            {
+                std::lock_guard<std::mutex> hold(st->use);
+                MarfProfScope ps("wgrad_fused", s);
+                HIPCHK(marf_launch_wgrad_fused(Lf, nf, p.S, (int)chunk, n_chunks, g, (const float*)(sv + p.c2f), net->L,
+                                               q.nk0w, d_gout, denom, s, st->s2, st->ev[0], st->ev[1]),
+                       "step_backward fused weight gradients");
+            }
+            for (int l = nl - 1; l >= 0; --l) {
+                rc = mark_layer(ev, l, s);
+                if (rc) return rc;
+            }
+            d_dparams = nullptr;  // done
+        }
+    }
     // the layers finish in reverse order (last layer first, layer 0 last), each marked by its event,
     // so that a bucketed all-reduce of finished layers overlaps the remaining weight gradients
     if (d_dparams) {

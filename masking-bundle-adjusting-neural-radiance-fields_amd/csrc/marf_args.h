@@ -155,6 +155,30 @@ hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev&
 hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
                              int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s,
                              const WgRange* rng = nullptr);
+// One layer of the fused weight-gradient launch (marf_launch_wgrad_fused): its split-K partials
+// [n_parts][M][K] (+ [n_parts][M] bias) and the fixed-order reduction into dW [Mo][Ko] / db [Mo].
+struct WgFusedLayer {
+    int kind;                 // 0: 256 x 256 LDS-DMA (hidden layer); 1: layer 0, feat_0 recomputed (256 x 96);
+                              // 2: layer 0 stored (marf_launch_wgrad's kernel); 3: reduction only
+    const void* dz;           // kinds 0..2: [S][ldz] bf16
+    const void* feat;         // kinds 0, 2: [S][ldf] bf16
+    int ldz, ldf, M, K;
+    float* partial;
+    float* bpartial;
+    int n_parts;              // partials to reduce (kinds 0..2: the launch's n_chunks)
+    int Mo, Ko;
+    float* dW;
+    float* db;
+    const int* kmap;          // layer 0: column of true input feature k in the partial
+};
+// every kind-0 layer's chunk products in one launch on s, the layer-0 one (kind 1 or 2) beside it on
+// s2 (fork / join events), then every layer's reduction in one launch on s; false if a shape does
+// not qualify
+bool marf_wgrad_fused_ok(const WgFusedLayer* layers, int n_layers, long long S, int chunk, int n_chunks,
+                         long long Np_pad);
+hipError_t marf_launch_wgrad_fused(const WgFusedLayer* layers, int n_layers, long long S, int chunk, int n_chunks,
+                                   const GeoDev& f0_geo, const float* c2f_w, int L, int nk0, const float* gscale,
+                                   const float* denom, hipStream_t s, hipStream_t s2, hipEvent_t fork, hipEvent_t join);
 hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* feat, long long S, int ldf, int K,
                                   int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s);
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,

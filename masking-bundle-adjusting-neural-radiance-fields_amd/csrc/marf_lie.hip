@@ -265,46 +265,54 @@ __global__ void k_sl3_backward(const float* __restrict__ h, const float* __restr
 }
 
 // Per-patch sum (fixed order, fp64) of the per-tile dH partials written by the backward MLP
-// kernel, then the Lie adjoint.  One 64-thread block per patch.
+// kernel, then the Lie adjoint.  One block per patch.
 // partial: [B * tiles_per_patch][9] fp32; dH_out: [B][9] (optional); dh: [B][8] (accumulate=0 ->
 // overwrite).
-__global__ void k_reduce_dH_lie_bwd(const float* __restrict__ partial, int tiles_per_patch,
+// 576 threads = 64 slots x 9 entries: the tile partials of a patch pass through LDS in segments of
+// 64 x RD_SEG tiles (every thread loads, all loads in flight together), and thread (t, e) adds entry
+// e of tiles t, t + 64, t + 128, ... in that order in fp64 -- the per-slot sums of the former 64-thread
+// form, which issued each slot's loads one after another (42 us at C3), in the same order.
+constexpr int RD_SEG = 16;
+__global__ __launch_bounds__(576) void k_reduce_dH_lie_bwd(const float* __restrict__ partial, int tiles_per_patch,
                                     const float* __restrict__ h, float* __restrict__ dH_out,
                                     float* __restrict__ dh, int batch_hint, const float* __restrict__ gscale,
                                     const float* __restrict__ denom) {
     __shared__ double red[64][9];
-    int b = blockIdx.x;
-    int t = threadIdx.x;
-    double acc[9];
-    for (int e = 0; e < 9; ++e) acc[e] = 0.0;
+    __shared__ float seg[64 * RD_SEG * 9];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int t = tid & 63, e = tid >> 6;
+    double acc = 0.0;
     const float* p = partial + (size_t)b * tiles_per_patch * 9;
-    // unrolled so the tile partials' loads are in flight together; per-entry order unchanged
-#pragma unroll 8
-    for (int i = t; i < tiles_per_patch; i += 64)
-#pragma unroll
-        for (int e = 0; e < 9; ++e) acc[e] += (double)p[(size_t)i * 9 + e];
-    for (int e = 0; e < 9; ++e) red[t][e] = acc[e];
+    for (int i0 = 0; i0 < tiles_per_patch; i0 += 64 * RD_SEG) {
+        const int n = min(64 * RD_SEG, tiles_per_patch - i0) * 9;
+        __syncthreads();  // the previous segment is consumed
+        for (int q = tid; q < n; q += 576) seg[q] = p[(size_t)i0 * 9 + q];
+        __syncthreads();
+        for (int k = 0; t + 64 * k < n / 9; ++k) acc += (double)seg[(t + 64 * k) * 9 + e];
+    }
+    red[t][e] = acc;
     __syncthreads();
     // the nine entries are summed on nine threads at once, each in the fixed order i = 0..63
     __shared__ float dHs[9];
-    if (t < 9) {
+    if (tid < 9) {
         double s = 0.0;
-        for (int i = 0; i < 64; ++i) s += red[i][t];
-        dHs[t] = (float)s;
+        for (int i = 0; i < 64; ++i) s += red[i][tid];
+        dHs[tid] = (float)s;
     }
     __syncthreads();
-    if (t == 0) {
+    if (tid == 0) {
         float dHf[9];
-        for (int e = 0; e < 9; ++e) dHf[e] = dHs[e];
+        for (int q = 0; q < 9; ++q) dHf[q] = dHs[q];
         // fused step: partials carry the unit-upstream gradient without 1/denominator
         if (gscale)
-            for (int e = 0; e < 9; ++e) dHf[e] = dHf[e] * (gscale[0] / denom[0]);
+            for (int q = 0; q < 9; ++q) dHf[q] = dHf[q] * (gscale[0] / denom[0]);
         if (dH_out)
-            for (int e = 0; e < 9; ++e) dH_out[9 * b + e] = dHf[e];
+            for (int q = 0; q < 9; ++q) dH_out[9 * b + q] = dHf[q];
         if (dh) {
             float d[8];
             sl3_backward_one(h + 8 * b, dHf, d, batch_hint);
-            for (int e = 0; e < 8; ++e) dh[8 * b + e] = d[e];
+            for (int q = 0; q < 8; ++q) dh[8 * b + q] = d[q];
         }
     }
 }
@@ -370,7 +378,7 @@ hipError_t marf_launch_reduce_dH(const float* partial, int tiles_per_patch, int 
                                  float* dH_out, float* dh, int batch_hint, hipStream_t s, const float* gscale,
                                  const float* denom) {
     if (B <= 0) return hipSuccess;
-    hipLaunchKernelGGL(marf::k_reduce_dH_lie_bwd, dim3(B), dim3(64), 0, s, partial, tiles_per_patch, h, dH_out, dh,
+    hipLaunchKernelGGL(marf::k_reduce_dH_lie_bwd, dim3(B), dim3(576), 0, s, partial, tiles_per_patch, h, dH_out, dh,
                        batch_hint, gscale, denom);
     return hipGetLastError();
 }

@@ -18,6 +18,7 @@ struct Pending {
 };
 std::mutex g_mu;
 bool g_on = false;
+std::string g_filter;  // ",name1,name2," or empty (every kernel)
 std::vector<Pending> g_pending;
 std::vector<hipEvent_t> g_pool;
 std::map<std::string, std::pair<double, long long>> g_acc;
@@ -39,6 +40,7 @@ bool marf_prof_on() { return g_on; }
 void* marf_prof_begin(const char* name, hipStream_t s) {
     if (!g_on) return nullptr;
     std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_filter.empty() && g_filter.find("," + std::string(name) + ",") == std::string::npos) return nullptr;
     Pending* p = new Pending{name, take(), take()};
     if (!p->a || !p->b) {
         delete p;
@@ -94,6 +96,13 @@ extern "C" {
 int marf_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_on = on != 0;
+    return 0;
+}
+
+int marf_profile_filter(const char* names) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_filter.clear();
+    if (names && names[0]) g_filter = "," + std::string(names) + ",";
     return 0;
 }
 

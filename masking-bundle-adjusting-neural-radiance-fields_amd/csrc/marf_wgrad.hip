@@ -15,6 +15,7 @@
 // 512 threads = 8 waves as 4 (rows) x 2 (cols); each wave owns RT x CT accumulator tiles.
 #include "marf_args.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -59,8 +60,10 @@ MARF_DEV i16x4 tr_read(const u16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
 }
 
+// the product of pixel chunk `chunk_id` into output block `ob` (the body of one k_wgrad block;
+// also a work item of k_wgrad_fused)
 template <class P, int RT, int CT, int SP>
-__global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
+MARF_DEV void wgrad_body(const WgArgs& a, int chunk_id, int ob, char* smem) {
     typedef typename P::T T;
     constexpr int BM = WgGeo<RT, CT>::BM, BN = WgGeo<RT, CT>::BN;
     constexpr int PADE = sizeof(T) == 2 ? 32 : 4;  // row padding (elements), keeps rows 16-B aligned
@@ -68,13 +71,10 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
     constexpr int VEC = 16 / sizeof(T);          // elements per 16-byte vector
     constexpr int NVZ = SP * BM / VEC / 512;     // dz vectors per thread and stage
     constexpr int NVF = SP * BN / VEC / 512;     // feat vectors per thread and stage
-    extern __shared__ __attribute__((aligned(16))) char smem[];
     T* tz = reinterpret_cast<T*>(smem);          // [SP][LDZ]
     T* tf = tz + SP * LDZ;                        // [SP][LDF]
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wr = wave >> 1, wc = wave & 1;
-    const int chunk_id = blockIdx.x;
-    const int ob = blockIdx.y;
     const int m0 = (ob / a.n_oblk_c) * BM, k0 = (ob % a.n_oblk_c) * BN;
     const long long s_begin = (long long)chunk_id * a.chunk;
     const long long s_end = min(s_begin + a.chunk, a.S);
@@ -207,6 +207,12 @@ __global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
     }
 }
 
+template <class P, int RT, int CT, int SP>
+__global__ __launch_bounds__(512, 1) void k_wgrad(WgArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    wgrad_body<P, RT, CT, SP>(a, blockIdx.x, blockIdx.y, smem);
+}
+
 // ---- bf16, 256 x 256 (or 256 x 96) output blocks: LDS-DMA ring
 // The same product with the operands streamed HBM -> LDS by global_load_lds_dwordx4 into an
 // NBUF-deep ring of SP-pixel stages, NBUF-2 stages in flight behind the one being consumed (the
@@ -229,6 +235,11 @@ MARF_DEV void glds16(const char* src, unsigned lds) {
 }
 
 constexpr int F0_PATCHES = 4;  // patches a layer-0 weight-gradient chunk may span (host-checked)
+// Ring shapes (same-box A/B, profiles/r4g, r4h): the hidden layers read 32-row stages of dz + feat
+// through a 4-deep ring (64-row stages, a 5-deep ring and non-temporal loads measured no faster);
+// the layer-0 gradient, which recomputes feat_0 and moves only dz over the ring, runs 64-row stages
+// 3 deep (0.65 -> 0.53 ms at C3: half the barriers per pixel).
+constexpr int WG_SPH = 32, WG_NBUF_H = 4, WG_SP0 = 64, WG_NBUF_0 = 3, WG_NBUF_96 = 4;
 
 MARF_DEV int swz(int r, int c) {  // byte offset of bf16 element (r, c) in a 256-wide swizzled stage
     return r * 512 + ((((c >> 3) ^ (4 * (r & 3)))) << 4) + (c & 7) * 2;
@@ -248,8 +259,10 @@ MARF_DEV int foff(int r, int c) {
     else return r * (KF * 2) + c * 2;
 }
 
+// chunk `chunk_id` into output block `ob` (the body of one k_wgrad_dma block; also a work item of
+// k_wgrad_fused)
 template <class P, int NBUF, int SP, int KF, bool F0 = false>
-__global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
+MARF_DEV void wgrad_dma_body(const WgArgs& a, int chunk_id, int ob, char* smem) {
     static_assert(KF == 256 || KF == 96, "feat width");
     static_assert(!F0 || (KF == 96 && SP % 32 == 0), "feat_0 recompute: the 96-wide layer-0 stage, 32-row blocks");
     constexpr int WR = KF == 256 ? 4 : 8, WC = 8 / WR;  // wave grid over the 256 x KF output
@@ -261,22 +274,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     static_assert(NGZ * 8192 == ZB && FB % 1024 == 0 && NBUF >= 2 && NBUF <= 6, "stage shape");
     constexpr int PER_ST = NGZ + NGF;            // vmcnt units per stage (the same on every wave)
     constexpr int STB = ZB + FB;                 // bytes of one ring slot
-    extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wr = wave / WC, wc = wave % WC;
-    // (chunk, output block): wider layers (M, K multiples of 256, e.g. 512) split the output in
-    // 256 x KF blocks.  The blocks sharing a chunk take ids 8 apart, i.e. the same XCD (blocks are
-    // dealt to the 8 XCDs round robin), so the second read of each operand slice hits its L2.
-    const int n_ob = (a.M / 256) * a.n_oblk_c;
-    int chunk_id, ob;
-    if (n_ob > 1 && a.n_chunks % 8 == 0) {
-        const int grp = blockIdx.x / (8 * n_ob), rem = blockIdx.x % (8 * n_ob);
-        chunk_id = grp * 8 + rem % 8;
-        ob = rem / 8;
-    } else {
-        chunk_id = blockIdx.x % a.n_chunks;
-        ob = blockIdx.x / a.n_chunks;
-    }
     const int m0 = (ob / a.n_oblk_c) * 256, k0 = (ob % a.n_oblk_c) * KF;
     long long s_begin, s_end;
     int pidx;  // the partial this block writes
@@ -487,6 +486,25 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     }
 }
 
+template <class P, int NBUF, int SP, int KF, bool F0 = false>
+__global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // (chunk, output block): wider layers (M, K multiples of 256, e.g. 512) split the output in
+    // 256 x KF blocks.  The blocks sharing a chunk take ids 8 apart, i.e. the same XCD (blocks are
+    // dealt to the 8 XCDs round robin), so the second read of each operand slice hits its L2.
+    const int n_ob = (a.M / 256) * a.n_oblk_c;
+    int chunk_id, ob;
+    if (n_ob > 1 && a.n_chunks % 8 == 0) {
+        const int grp = blockIdx.x / (8 * n_ob), rem = blockIdx.x % (8 * n_ob);
+        chunk_id = grp * 8 + rem % 8;
+        ob = rem / 8;
+    } else {
+        chunk_id = blockIdx.x % a.n_chunks;
+        ob = blockIdx.x / a.n_chunks;
+    }
+    wgrad_dma_body<P, NBUF, SP, KF, F0>(a, chunk_id, ob, smem);
+}
+
 // Last layer (3 outputs): dW[c][k] = sum_px g[px][c] feat[px][k], db[c] = sum_px g[px][c].
 // Bandwidth-bound (reads feat_{n-1} once): each thread owns VEC consecutive features (one 16-byte
 // load per pixel row) and a pixel lane; a wave covers whole rows so every load instruction is
@@ -555,17 +573,81 @@ __global__ __launch_bounds__(256) void k_wgrad_last(const float* __restrict__ gl
     }
 }
 
-// Fixed-order sum of the chunk partials into the flat fp32 gradient (nn.Linear layout [M][K],
-// unpadded [Mo][Ko]), then the bias, optionally times gscale / denom (device scalars).  Block = 64 outputs x 4 chunk groups; group g sums chunks
-// [g*n/4, (g+1)*n/4) with independent loads in flight, the 4 group sums are added in order.
-__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ partial,
-                                                      const float* __restrict__ bpartial, int n_chunks, int M, int K,
-                                                      int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db,
-                                                      const float* __restrict__ gscale, const float* __restrict__ denom,
-                                                      const int* __restrict__ kmap) {
-    __shared__ float red[4][64];
+// First stage of a reduction over many partials (the fused step writes one per pixel tile): group
+// g sums chunks [g*per, (g+1)*per) of partial [n][E] (and bpartial [n][Eb]) into out [G][E]
+// (bout [G][Eb]), in chunk order.  Coalesced over the element index.
+__global__ __launch_bounds__(256) void k_fold_partials(const float* __restrict__ partial, const float* __restrict__ bpartial,
+                                                       int n, int per, long long E, int Eb, float* __restrict__ out,
+                                                       float* __restrict__ bout) {
+    const long long e = blockIdx.x * 256LL + threadIdx.x;
+    const int g = blockIdx.y;
+    const int c0 = g * per, c1 = min(n, c0 + per);
+    if (e < E) {
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        int c = c0;
+        // 2 x 4 loads in flight; acc[u] still sums chunks u, u+4, u+8, ... in order
+#pragma unroll 2
+        for (; c + 4 <= c1; c += 4)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] += partial[(size_t)(c + u) * E + e];
+        for (int u = 0; c < c1; ++c, ++u) acc[u] += partial[(size_t)c * E + e];
+        out[(size_t)g * E + e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    } else if (e < E + Eb) {
+        const int eb = (int)(e - E);
+        float s = 0.f;
+        for (int c = c0; c < c1; ++c) s += bpartial[(size_t)c * Eb + eb];
+        bout[(size_t)g * Eb + eb] = s;
+    }
+}
+
+
+// ---- the weight gradients of a step in three launches (marf_launch_wgrad_fused)
+//
+// The per-layer path is 4 + 5 launches per step (three hidden layers, layer 0, five reductions),
+// each with its own ramp and tail, layer 0 (sin / cos bound: it recomputes feat_0) after the hidden
+// layers (HBM bound).  Here: every hidden layer's chunks in ONE launch (k_wgrad_dma_layers), layer 0
+// in a concurrent launch on a second stream (its blocks take CUs as the hidden-layer blocks free
+// them), then every layer's reduction in ONE launch (k_wgrad_reduce_layers).  Each block runs the
+// per-layer kernels' own body for its (layer, chunk) and the reduction the arithmetic of
+// k_wgrad_reduce, so every partial and every gradient is bit-identical to the per-layer path.
+// (One persistent work-queue kernel holding both bodies needed 256 VGPRs and spilled; separate
+// kernels keep each body's own allocation.)
+constexpr int WF_MAXJ = 6;  // the pixel-per-wave step: at most 5 layers + the last-layer reduction
+
+struct WgLayersArgs {
+    WgArgs a[WF_MAXJ];
+    int n_chunks;
+};
+
+template <class P, int NBUF, int SP, int KF>
+__global__ __launch_bounds__(512, 1) void k_wgrad_dma_layers(WgLayersArgs la) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int l = blockIdx.x / la.n_chunks, c = blockIdx.x - l * la.n_chunks;  // layer-major
+    wgrad_dma_body<P, NBUF, SP, KF>(la.a[l], c, 0, smem);
+}
+
+struct WgRedJob {
+    const float* partial;
+    const float* bpartial;
+    int n_chunks, M, K, Mo, Ko, blk0;
+    float* dW;
+    float* db;
+    const int* kmap;
+};
+struct WgRedArgs {
+    WgRedJob job[WF_MAXJ];
+    int n_jobs;
+    const float* gscale;
+    const float* denom;
+};
+
+// k_wgrad_reduce's block (64 outputs x 4 chunk groups) for output block `blk` of one job
+MARF_DEV void wgrad_reduce_block(const float* __restrict__ partial, const float* __restrict__ bpartial, int n_chunks,
+                                 int M, int K, int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db,
+                                 const float* __restrict__ gscale, const float* __restrict__ denom,
+                                 const int* __restrict__ kmap, int blk, float (*red)[64]) {
     const long long n = (long long)Mo * Ko;
-    const long long e = blockIdx.x * 64LL + (threadIdx.x & 63);
+    const long long e = blk * 64LL + (threadIdx.x & 63);
     const int g = threadIdx.x >> 6;
     const int c0 = (int)((long long)n_chunks * g / 4), c1 = (int)((long long)n_chunks * (g + 1) / 4);
     float s = 0.f;
@@ -601,31 +683,26 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
     }
 }
 
-// First stage of a reduction over many partials (the fused step writes one per pixel tile): group
-// g sums chunks [g*per, (g+1)*per) of partial [n][E] (and bpartial [n][Eb]) into out [G][E]
-// (bout [G][Eb]), in chunk order.  Coalesced over the element index.
-__global__ __launch_bounds__(256) void k_fold_partials(const float* __restrict__ partial, const float* __restrict__ bpartial,
-                                                       int n, int per, long long E, int Eb, float* __restrict__ out,
-                                                       float* __restrict__ bout) {
-    const long long e = blockIdx.x * 256LL + threadIdx.x;
-    const int g = blockIdx.y;
-    const int c0 = g * per, c1 = min(n, c0 + per);
-    if (e < E) {
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        int c = c0;
-        // 2 x 4 loads in flight; acc[u] still sums chunks u, u+4, u+8, ... in order
-#pragma unroll 2
-        for (; c + 4 <= c1; c += 4)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] += partial[(size_t)(c + u) * E + e];
-        for (int u = 0; c < c1; ++c, ++u) acc[u] += partial[(size_t)c * E + e];
-        out[(size_t)g * E + e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    } else if (e < E + Eb) {
-        const int eb = (int)(e - E);
-        float s = 0.f;
-        for (int c = c0; c < c1; ++c) s += bpartial[(size_t)c * Eb + eb];
-        bout[(size_t)g * Eb + eb] = s;
-    }
+__global__ __launch_bounds__(256) void k_wgrad_reduce_layers(WgRedArgs r) {
+    __shared__ float red[4][64];
+    int j = 0;
+    while (j < r.n_jobs - 1 && (int)blockIdx.x >= r.job[j + 1].blk0) ++j;
+    const WgRedJob& q = r.job[j];
+    wgrad_reduce_block(q.partial, q.bpartial, q.n_chunks, q.M, q.K, q.Mo, q.Ko, q.dW, q.db, r.gscale, r.denom, q.kmap,
+                       (int)blockIdx.x - q.blk0, red);
+}
+
+// Fixed-order sum of the chunk partials into the flat fp32 gradient (nn.Linear layout [M][K],
+// unpadded [Mo][Ko]), then the bias, optionally times gscale / denom (device scalars).  Block = 64
+// outputs x 4 chunk groups; group g sums chunks [g*n/4, (g+1)*n/4) with independent loads in
+// flight, the 4 group sums are added in order (wgrad_reduce_block).
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ partial,
+                                                      const float* __restrict__ bpartial, int n_chunks, int M, int K,
+                                                      int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db,
+                                                      const float* __restrict__ gscale, const float* __restrict__ denom,
+                                                      const int* __restrict__ kmap) {
+    __shared__ float red[4][64];
+    wgrad_reduce_block(partial, bpartial, n_chunks, M, K, Mo, Ko, dW, db, gscale, denom, kmap, blockIdx.x, red);
 }
 
 }  // namespace marf
@@ -652,12 +729,6 @@ static bool wgrad_dma_enabled() {
     const char* e = getenv("MARF_WGRAD_DMA");  // A/B switch (read per launch): 0 = register-staged kernel
     return !(e && e[0] == '0');
 }
-
-// Ring shapes (same-box A/B, profiles/r4g, r4h): the hidden layers read 32-row stages of dz + feat
-// through a 4-deep ring (64-row stages, a 5-deep ring and non-temporal loads measured no faster);
-// the layer-0 gradient, which recomputes feat_0 and moves only dz over the ring, runs 64-row stages
-// 3 deep (0.65 -> 0.53 ms at C3: half the barriers per pixel).
-constexpr int WG_SPH = 32, WG_NBUF_H = 4, WG_SP0 = 64, WG_NBUF_0 = 3, WG_NBUF_96 = 4;
 
 template <class P, int KF, bool F0 = false>
 static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
@@ -775,6 +846,117 @@ hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev&
     a.partial = partial;
     a.bpartial = bpartial;
     return launch_wg_dma<PrecBF16, 96, true>(a, n_chunks, s);
+}
+
+// ---- the fused launch: hidden layers in one launch, layer 0 beside it on `s2`, one reduction launch
+bool marf_wgrad_fused_ok(const WgFusedLayer* layers, int n_layers, long long S, int chunk, int n_chunks,
+                         long long Np_pad) {
+    if (!layers || n_layers < 1 || n_layers > WF_MAXJ || n_chunks < 1 || chunk < 64 || chunk % 64) return false;
+    if (const char* e = getenv("MARF_WGRAD_FUSED")) {  // A/B switch (read per launch): 0 = per-layer launches
+        if (e[0] == '0') return false;
+    }
+    int n_l0 = 0;
+    for (int i = 0; i < n_layers; ++i) {
+        const WgFusedLayer& L = layers[i];
+        if (L.Mo > L.M || L.Ko > L.K || !L.partial || !L.bpartial || !L.dW || !L.db) return false;
+        switch (L.kind) {
+            case 0:  // k_wgrad_dma<PrecBF16, 4, 32, 256>'s one-output-block shape (marf_launch_wgrad's dma256)
+                if (!(L.M == 256 && L.K == 256 && L.ldz % 8 == 0 && L.ldz >= L.M && L.ldf % 8 == 0 && L.ldf >= L.K &&
+                      S % WG_SPH == 0 && chunk % WG_SPH == 0 && wgrad_dma_enabled()))
+                    return false;
+                break;
+            case 1:  // marf_launch_wgrad_l0_recompute's shape
+                if (!(L.K == 96 && marf_wgrad_l0_recompute_ok(L.M, L.ldz, 96, S, chunk, n_chunks, Np_pad))) return false;
+                ++n_l0;
+                break;
+            case 2:  // layer 0 stored: any shape marf_launch_wgrad takes (its kernel is picked there)
+                ++n_l0;
+                break;
+            case 3:
+                if (L.n_parts < 1 || L.n_parts > 1024) return false;  // (the per-layer path folds above 1024)
+                break;
+            default: return false;
+        }
+    }
+    return n_l0 <= 1;
+}
+
+hipError_t marf_launch_wgrad_fused(const WgFusedLayer* layers, int n_layers, long long S, int chunk, int n_chunks,
+                                   const GeoDev& f0_geo, const float* c2f_w, int L, int nk0, const float* gscale,
+                                   const float* denom, hipStream_t s, hipStream_t s2, hipEvent_t fork,
+                                   hipEvent_t join) {
+    hipError_t e;
+    // layer 0 on s2, beside the hidden layers
+    const WgFusedLayer* l0 = nullptr;
+    for (int i = 0; i < n_layers; ++i)
+        if (layers[i].kind == 1 || layers[i].kind == 2) l0 = &layers[i];
+    if (l0) {
+        if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(s2, fork, 0)) != hipSuccess) return e;
+        if (l0->kind == 1)
+            e = marf_launch_wgrad_l0_recompute(l0->dz, l0->ldz, f0_geo, c2f_w, L, nk0, S, l0->M, chunk, n_chunks, l0->partial,
+                                               l0->bpartial, s2);
+        else
+            e = marf_launch_wgrad(1, l0->dz, l0->ldz, l0->feat, l0->ldf, S, l0->M, l0->K, chunk, n_chunks, l0->partial,
+                                  l0->bpartial, s2);
+        if (e != hipSuccess) return e;
+        if ((e = hipEventRecord(join, s2)) != hipSuccess) return e;
+    }
+    // every hidden layer's chunks: one launch, layer-major blocks
+    WgLayersArgs la;
+    memset(&la, 0, sizeof(la));
+    la.n_chunks = n_chunks;
+    int nh = 0;
+    for (int i = 0; i < n_layers; ++i) {
+        const WgFusedLayer& Ly = layers[i];
+        if (Ly.kind != 0) continue;
+        WgArgs& a = la.a[nh++];
+        a.dz = Ly.dz;
+        a.feat = Ly.feat;
+        a.S = S;
+        a.ldz = Ly.ldz;
+        a.ldf = Ly.ldf;
+        a.M = Ly.M;
+        a.K = Ly.K;
+        a.chunk = chunk;
+        a.n_chunks = n_chunks;
+        a.n_oblk_c = 1;
+        a.partial = Ly.partial;
+        a.bpartial = Ly.bpartial;
+    }
+    if (nh) {
+        const size_t lds = (size_t)WG_NBUF_H * WG_SPH * (512 + 256 * 2);
+        typedef PrecBF16 P;
+        e = ensure_dynamic_lds((const void*)k_wgrad_dma_layers<P, WG_NBUF_H, WG_SPH, 256>, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((k_wgrad_dma_layers<P, WG_NBUF_H, WG_SPH, 256>), dim3(nh * n_chunks), dim3(512), lds, s, la);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (l0 && (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
+    // every layer's reduction: one launch, in the layers' order
+    WgRedArgs r;
+    memset(&r, 0, sizeof(r));
+    r.n_jobs = n_layers;
+    r.gscale = gscale;
+    r.denom = denom;
+    int blk = 0;
+    for (int i = 0; i < n_layers; ++i) {
+        const WgFusedLayer& Ly = layers[i];
+        WgRedJob& q = r.job[i];
+        q.partial = Ly.partial;
+        q.bpartial = Ly.bpartial;
+        q.n_chunks = Ly.kind == 3 ? Ly.n_parts : n_chunks;
+        q.M = Ly.M;
+        q.K = Ly.K;
+        q.Mo = Ly.Mo;
+        q.Ko = Ly.Ko;
+        q.dW = Ly.dW;
+        q.db = Ly.db;
+        q.kmap = Ly.kmap;
+        q.blk0 = blk;
+        blk += (int)(((long long)Ly.Mo * Ly.Ko + Ly.Mo + 63) / 64);
+    }
+    hipLaunchKernelGGL(k_wgrad_reduce_layers, dim3(blk), dim3(256), 0, s, r);
+    return hipGetLastError();
 }
 
 hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* feat, long long S, int ldf, int K, int chunk,

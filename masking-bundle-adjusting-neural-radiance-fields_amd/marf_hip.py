@@ -83,6 +83,7 @@ _SIGS = {
     "marf_debug_set_stamps": (None, [_c_vp]),
     "marf_profile_enable": (_c_int, [_c_int]),
     "marf_profile_reset": (_c_int, []),
+    "marf_profile_filter": (_c_int, [ctypes.c_char_p]),
     "marf_profile_read": (_c_int, [ctypes.c_char_p, _c_int, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_ll), _c_int]),
 }
 
@@ -173,6 +174,11 @@ def profile_enable(on=True):
 
 def profile_reset():
     _check(lib().marf_profile_reset())
+
+
+def profile_filter(names=None):
+    """Time only the kernels named (profile names, e.g. ["mlp_step"]); None = every kernel."""
+    _check(lib().marf_profile_filter(",".join(names).encode() if names else None))
 
 
 def profile_read():
