@@ -236,7 +236,9 @@ class Model(torch.nn.Module):
         """One optimisation step in the reference's order (model/planar.py:187-209)."""
         t_start = time.time()
         log_now = (self.it + 1) % self.opt.freq.scalar == 0
-        self.graph.need_edges = bool(self.opt.use_edges and log_now)
+        # the edge term is evaluated every step, as the reference's Graph.forward does
+        # (model/planar.py:336, 366-369): it carries no gradient, but loss.render / loss.all hold it
+        self.graph.need_edges = bool(self.opt.use_edges)
         self.optim.zero_grad()
         var = self.graph.forward(var, mode="train")
         loss = self.graph.compute_loss(var, mode="train")
@@ -425,7 +427,7 @@ class Graph(torch.nn.Module):
                         edge_loss = (diff ** 2).sum() / (self.batch_size * diff[0].numel())
                     else:
                         edge_loss = self.mse_loss(var.edge_prediction, imgs.edges[b0:b1], me)
-                else:  # edges are evaluated at logging steps only (they carry no gradient)
+                else:  # no edge maps (a caller that turned need_edges off, or no edge targets)
                     edge_loss = torch.zeros((), dtype=torch.float64, device=rgb_loss.device)
             else:
                 edge_loss = torch.tensor(0)

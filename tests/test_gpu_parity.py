@@ -237,6 +237,42 @@ def c1_setup(precision, tmp_path, seed=3):
     return m, edict(idx=torch.arange(5), images=m.images)
 
 
+def test_edge_term_every_step(tmp_path):
+    """The edge term is evaluated at every training step, as the reference's Graph.forward +
+    compute_loss do (model/planar.py:336, 366-380): on a step that is not a logging step, loss.edge is
+    the masked MSE between the edge maps of the prediction and of the gray targets (the oracle's
+    restatement of inputs.compute_edges, float64), and loss.render = (1 - alpha) rgb + alpha edge with
+    alpha = it / max_iter.  The gradients do not depend on it (the edge term carries none)."""
+    from model import planar
+    from util import EasyDict as edict
+    import time
+    imgs = g("cat_batch3_c1")
+    opt = make_opt(tmp_path, precision="fp32", max_iter=40)
+    torch.manual_seed(3)
+    m = planar.Model(opt)
+    rgb = t(imgs["rgb"].astype(np.float32) / np.float32(255))
+    mask = t(imgs["mask"].astype(np.float32))
+    gray = rgb.mean(1, keepdim=True)  # any single-channel target image serves the check
+    import inputs
+    edges = inputs.compute_edges(gray, DEV)
+    me = inputs.erode_images(mask, DEV)
+    m.images = edict(rgb=rgb, masks=mask, masks_eroded=me, edges=edges, gt_hom=None, gt=None)
+    m.build_networks()
+    m.setup_optimizer()
+    m.timer = edict(start=time.time(), it_mean=None)
+    var = edict(idx=torch.arange(5), images=m.images)
+    for step in range(3):  # freq.scalar = 20: none of these is a logging step
+        loss = m.train_iteration(var, _Loader())
+        pred = var.rgb_prediction_map.detach().cpu().numpy()
+        B, C, H, W = pred.shape
+        e_pred = oracle.edge_map(pred.reshape(B * C, H, W)).reshape(B, C, H, W)
+        mm = me.cpu().numpy().astype(np.float64)
+        ref = (((e_pred - edges.cpu().numpy()) * mm) ** 2).sum() / (mm.sum() * 3)
+        assert float(loss.edge) > 0 and abs(float(loss.edge) / ref - 1) <= 1e-9, (step, float(loss.edge), ref)
+        alpha = step / opt.max_iter  # compute_loss's it before its increment
+        np.testing.assert_allclose(float(loss.render), (1 - alpha) * float(loss.rgb) + alpha * ref, rtol=1e-6)
+
+
 def test_c1_real_init_and_trajectory_fp32(tmp_path):
     z = g("step_c1")
     m, var = c1_setup("fp32", tmp_path)
