@@ -6,8 +6,11 @@ free of diagnostic switches):  python tools/ab_variant.py NAME [NAME ...]  ->  l
   nosave         k_step2 without its saved-tensor stores (feat_l, dz_l) and their vmcnt accounting
   nodma_nosave   both
 
-Their results are wrong on purpose: bench them with MARF_AB_TIMING_ONLY=1 and MARF_LIB=<the .so>
-(bench.py then never reports the line as a headline)."""
+  dmant / stnt / stsc1 / dmant_stnt   cache-policy bits on the weight DMA / the saved-tensor stores
+                 (correct results, the same bits)
+
+The first three compute wrong results on purpose: bench them with MARF_AB_TIMING_ONLY=1 and
+MARF_LIB=<the .so> (bench.py then never reports the line as a headline)."""
 import os
 import shutil
 import sys
@@ -30,6 +33,14 @@ PATCHES = {
     "nosave": [("marf_step2.hip", SAVE, "        (void)row0; (void)f0; (void)f1; (void)contig;\n")],
 }
 PATCHES["nodma_nosave"] = PATCHES["nodma"] + PATCHES["nosave"]
+# cache-policy variants (correct results, same bits): the weight-ring DMA and / or the saved-tensor
+# stores with the nt (streaming) or sc1 (write-through) policy bits
+DMA_OP = "global_load_lds_dwordx4 %1, off offset:%3"
+ST_OP = "global_store_dwordx4 %0, %1, off offset:%2"
+PATCHES["dmant"] = [("marf_step2.hip", DMA_OP, DMA_OP + " nt")]
+PATCHES["stnt"] = [("marf_step2.hip", ST_OP, ST_OP + " nt")]
+PATCHES["stsc1"] = [("marf_step2.hip", ST_OP, ST_OP + " sc1")]
+PATCHES["dmant_stnt"] = PATCHES["dmant"] + PATCHES["stnt"]
 
 
 def build(name):
