@@ -224,6 +224,9 @@ def main():
     ap.add_argument("--cpu-sample-patches", type=int, default=4)
     ap.add_argument("--no-render", action="store_true",
                     help="skip the forward-only render rate (PMC passes: its launches share the step kernel's name)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay forward + loss + backward as one captured HIP graph (Model.captured_step); "
+                         "the per-kernel times and the roofline then come from eager steps")
     ap.add_argument("--launch-check", action="store_true",
                     help="set up the ranks and print the JSON line's world size / backend only (no GPU work)")
     args = ap.parse_args()
@@ -292,15 +295,17 @@ def main():
     b0, b1 = graph.shard if graph.shard else (0, B_total)
     px_local = (b1 - b0) * h * w
 
-    def step():
-        m.optim.zero_grad()
-        v = graph.forward(var, mode="train")
-        loss = graph.compute_loss(v, mode="train")
-        total = 0.
-        for key in loss:  # Model.summarize_loss without its host-side NaN asserts
-            if opt.loss_weight[key] is not None:
-                total = total + 10 ** float(opt.loss_weight[key]) * loss[key]
-        total.backward()
+    if args.graph and not m.graph_capable():
+        raise SystemExit("--graph: the step cannot be captured here (one process, use_edges off)")
+
+    def step(eager=False):
+        if args.graph and not eager:
+            v, loss = m.captured_step(var)
+        else:
+            m.optim.zero_grad()
+            v = graph.forward(var, mode="train")
+            loss = m._loss_sum(graph.compute_loss(v, mode="train"))  # summarize_loss without host syncs
+            loss.all.backward()
         m.all_reduce_grads()
         m.optim.step()
         graph.neural_image.progress.data.fill_(0.2)  # keep c2f partially on
@@ -329,16 +334,19 @@ def main():
     elapsed = time.perf_counter() - t0
     marf_hip.profile_enable(False)
     prof = marf_hip.profile_read()
-    # per-kernel breakdown: a separate pass of the same step with every kernel timed
+    # per-kernel breakdown: a separate pass of the same step with every kernel timed (eager: a
+    # replayed graph records no events)
     n_break = max(3, args.steps // 4)
     marf_hip.profile_reset()
     marf_hip.profile_filter(None)
     marf_hip.profile_enable(True)
     for _ in range(n_break):
-        step()
+        step(eager=True)
     barrier()
     marf_hip.profile_enable(False)
     prof_all = marf_hip.profile_read()
+    if args.graph:  # the dominant kernel's duration from the eager steps
+        prof = {k: (v[0] * args.steps / n_break, v[1] * args.steps // n_break) for k, v in prof_all.items()}
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -433,8 +441,11 @@ def main():
         "dist": dist,
         "kernels": per_kernel,
         "kernel_ms_per_step": step_kernel_ms,
-        "kernels_note": f"per-kernel HIP-event durations from {n_break} further steps with every kernel timed "
-                        "(the timed region times the dominant kernel only)",
+        "kernels_note": f"per-kernel HIP-event durations from {n_break} further eager steps with every kernel "
+                        "timed (the timed region times the dominant kernel only"
+                        + ("; with --graph it replays a captured graph and the roofline uses these eager steps)"
+                           if args.graph else ")"),
+        "graph": bool(args.graph),
     }
     if timing_only:
         out["timing_only"] = True  # never a headline: the build under test computes wrong results

@@ -72,6 +72,7 @@ class Model(torch.nn.Module):
         self.rank = torch.distributed.get_rank() if _dist() else 0
         self.world = torch.distributed.get_world_size() if _dist() else 1
         self.exchange_counts = {"bucketed": 0, "flat": 0}  # which gradient exchange each step took
+        self._step_graph = None  # (HIP graph, var, loss) of captured_step
 
     # ------------------------------------------------------------------ data
     def load_dataset(self):
@@ -176,6 +177,69 @@ class Model(torch.nn.Module):
         loss.update(all=loss_all)
         return loss
 
+    def _loss_sum(self, loss):
+        """summarize_loss's weighted sum without its host-side NaN / Inf asserts (each one waits for
+        the GPU: a captured step must not synchronise; train_iteration checks at logging steps)."""
+        loss_all = 0.
+        for key in loss:
+            if self.opt.loss_weight[key] is not None:
+                loss_all += 10 ** float(self.opt.loss_weight[key]) * loss[key]
+        loss.update(all=loss_all)
+        return loss
+
+    def graph_capable(self):
+        """A step can be captured when it has no host-dependent value per step: one process, the
+        fused step, no edge term (its alpha = it / max_iter is a host value)."""
+        return (self.world == 1 and not self.opt.use_edges and self.opt.get("fused_step", True)
+                and str(self.opt.device).startswith("cuda"))
+
+    def captured_step(self, var):
+        """Graph.forward + compute_loss + the weighted loss sum + backward of one training step as a
+        replayed HIP graph (torch.cuda.CUDAGraph).  The first call runs two eager warm-up passes (every
+        buffer and kernel attribute set up) and records the step once; every call replays the
+        recorded launches -- the same kernels on the same buffers with the same arguments, so the
+        same bits as the eager step (test_captured_step_matches_eager) without the per-launch host
+        work.  The weight repack is always recorded (the optimizer updates the weights between
+        replays), the optimizer step, progress update and fix_first stay eager (host values).
+        Returns (var, loss) with the graph's static tensors."""
+        if self._step_graph is None:
+            if not self.graph_capable():
+                raise RuntimeError("captured_step: needs one process, the fused step and use_edges off")
+            dev = torch.device(self.opt.device)
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    self.optim.zero_grad(set_to_none=True)
+                    v = self.graph.forward(var, mode="train")
+                    self._loss_sum(self.graph.compute_loss(v, mode="train")).all.backward()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self._drop_autograd(var)  # (no warm-up graph, whose gradient nodes live on `side`, stays alive)
+            self.graph.neural_image.engine(dev)._packed_version = None  # the repack must be recorded
+            self.optim.zero_grad(set_to_none=True)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                v = self.graph.forward(var, mode="train")
+                loss = self._loss_sum(self.graph.compute_loss(v, mode="train"))
+                loss.all.backward()
+            # the static outputs, detached: the recorded autograd graph is not needed after capture
+            for k in list(loss.keys()):
+                if torch.is_tensor(loss[k]):
+                    loss[k] = loss[k].detach()
+            self._drop_autograd(v)
+            self._step_graph = (g, v, loss)
+        g, v, loss = self._step_graph
+        g.replay()
+        return v, loss
+
+    @staticmethod
+    def _drop_autograd(var):
+        """Detach the prediction fields of a var bundle (their autograd graph is released)."""
+        for k in ("rgb_prediction", "rgb_prediction_map", "edge_prediction"):
+            if torch.is_tensor(var.get(k)):
+                var[k] = var[k].detach()
+        var.fused_loss = None
+
     def _grad_engine(self):
         """The neural image's engine, with per-layer gradient events armed for a bucketed exchange
         (MARF_GRAD_BUCKETS=0: the flat all-reduce after the whole backward)."""
@@ -239,11 +303,16 @@ class Model(torch.nn.Module):
         # the edge term is evaluated every step, as the reference's Graph.forward does
         # (model/planar.py:336, 366-369): it carries no gradient, but loss.render / loss.all hold it
         self.graph.need_edges = bool(self.opt.use_edges)
-        self.optim.zero_grad()
-        var = self.graph.forward(var, mode="train")
-        loss = self.graph.compute_loss(var, mode="train")
-        loss = self.summarize_loss(loss)
-        loss.all.backward()
+        if self.opt.get("cuda_graph") and self.graph_capable():
+            var, loss = self.captured_step(var)
+            if log_now:
+                self.summarize_loss({k: v for k, v in loss.items() if k != "all"})  # the NaN / Inf asserts
+        else:
+            self.optim.zero_grad()
+            var = self.graph.forward(var, mode="train")
+            loss = self.graph.compute_loss(var, mode="train")
+            loss = self.summarize_loss(loss)
+            loss.all.backward()
         self.all_reduce_grads()
         self.optim.step()
         if self.sched:

@@ -273,6 +273,41 @@ def test_edge_term_every_step(tmp_path):
         np.testing.assert_allclose(float(loss.render), (1 - alpha) * float(loss.rgb) + alpha * ref, rtol=1e-6)
 
 
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+def test_captured_step_matches_eager(precision, tmp_path):
+    """Model.captured_step (forward + loss + backward recorded once as a HIP graph and replayed,
+    opt.cuda_graph) against the eager step on the C1 batch, use_edges off: after 5 training
+    iterations (Adam, progress, fix_first between replays) the losses, warps and every MLP weight
+    are bit-identical, and the recorded weight repack follows the optimizer's updates."""
+    from model import planar
+    from util import EasyDict as edict
+    import time
+    imgs = g("cat_batch3_c1")
+    res = {}
+    for mode in ("eager", "graph"):
+        opt = make_opt(tmp_path / mode, precision=precision, use_edges=False, cuda_graph=(mode == "graph"))
+        torch.manual_seed(3)
+        m = planar.Model(opt)
+        rgb = t(imgs["rgb"].astype(np.float32) / np.float32(255))
+        mask = t(imgs["mask"].astype(np.float32))
+        m.images = edict(rgb=rgb, masks=mask, masks_eroded=mask, edges=None, gt_hom=None, gt=None)
+        m.build_networks()
+        m.setup_optimizer()
+        m.timer = edict(start=time.time(), it_mean=None)
+        var = edict(idx=torch.arange(5), images=m.images)
+        losses = []
+        for _ in range(5):
+            losses.append(float(m.train_iteration(var, _Loader()).rgb))
+            m.graph.warp_param.weight.data[0] = 0
+        assert (m._step_graph is not None) == (mode == "graph")
+        res[mode] = (losses, m.graph.warp_param.weight.detach().cpu(),
+                     [p.detach().cpu() for p in m.graph.neural_image.mlp.parameters()])
+    (la, wa, pa), (lb, wb, pb) = res["eager"], res["graph"]
+    assert la == lb, (la, lb)
+    assert torch.equal(wa.view(torch.int32), wb.view(torch.int32))
+    assert all(torch.equal(a.view(torch.int32), b.view(torch.int32)) for a, b in zip(pa, pb))
+
+
 def test_c1_real_init_and_trajectory_fp32(tmp_path):
     z = g("step_c1")
     m, var = c1_setup("fp32", tmp_path)
