@@ -114,6 +114,12 @@ int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** 
 /* As marf_net_create, with the pixels one fused step will process on this GPU (0 = unknown; kept for
  * size-dependent kernel choices: the split recipe runs k_step2 at every size today). */
 int marf_net_create_hint(int n_layers, const int* dims, int L, int dtype, long long pixels_hint, marf_net** out);
+/* As marf_net_create_hint, with skip connections (model/planar.py:419-420, 440-441; opt.arch.skip):
+ * bit l of skip_mask makes layer l's input [previous layer's output ; posenc features] (k_in =
+ * dims[l] + dims[0] in the flat parameter layout).  Hidden layers 1 .. n_layers-2 only, dims[l] a
+ * multiple of 32; the tile kernels (fp32, bf16, fp16) run such nets, the split-bf16 recipe refuses them. */
+int marf_net_create_skip(int n_layers, const int* dims, int L, int dtype, long long pixels_hint, unsigned skip_mask,
+                         marf_net** out);
 void marf_net_destroy(marf_net* net);
 long long marf_net_param_count(const marf_net* net);
 size_t marf_net_packed_bytes(const marf_net* net);

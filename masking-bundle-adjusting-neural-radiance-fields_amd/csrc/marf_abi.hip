@@ -59,6 +59,8 @@ struct Step2NetPlan {
 
 struct marf_net {
     int n_layers, L, D, dtype;
+    unsigned skip;  // bit l: layer l's input is [feature ; posenc] (model/planar.py:419-420, 440-441)
+    int kin[MARF_MAX_LAYERS];  // true input width of layer l (dims[l], + D for a skip layer)
     int kdt;  // kernel arithmetic of the generic kernels: 0 fp32, 1 bf16 (MARF_BF16 and MARF_BF16X3), 2 fp16
     Step2NetPlan s2;
     int dims[MARF_MAX_LAYERS + 1];
@@ -111,7 +113,7 @@ static void plan_step2_net(marf_net* n, long long pixels_hint) {
     memset(&q, 0, sizeof(q));
     q.variant = -1;
     const int nl = n->n_layers;
-    if (n->kdt != 1 || nl < 2 || nl > 5 || n->L > 32) return;
+    if (n->kdt != 1 || nl < 2 || nl > 5 || n->L > 32 || n->skip) return;  // (skip nets: the tile kernels)
     for (int l = 0; l < nl - 1; ++l)
         if (n->Mp[l] > 256) return;
     // decided once, here: the split recipe always runs this kernel; plain bf16 only on request
@@ -349,10 +351,15 @@ int marf_prologue_probe(const marf_geometry* geo, const marf_c2f* c2f, int L, co
 // ------------------------------------------------------------------ network
 
 int marf_net_create(int n_layers, const int* dims, int L, int dtype, marf_net** out) {
-    return marf_net_create_hint(n_layers, dims, L, dtype, 0, out);
+    return marf_net_create_skip(n_layers, dims, L, dtype, 0, 0u, out);
 }
 
 int marf_net_create_hint(int n_layers, const int* dims, int L, int dtype, long long pixels_hint, marf_net** out) {
+    return marf_net_create_skip(n_layers, dims, L, dtype, pixels_hint, 0u, out);
+}
+
+int marf_net_create_skip(int n_layers, const int* dims, int L, int dtype, long long pixels_hint, unsigned skip_mask,
+                         marf_net** out) {
     if (!out || !dims) return fail(MARF_ERR_INVALID, "net_create: NULL argument");
     *out = nullptr;
     if (n_layers < 2 || n_layers > MARF_MAX_LAYERS)
@@ -378,12 +385,34 @@ int marf_net_create_hint(int n_layers, const int* dims, int L, int dtype, long l
         }
         n->dims[i] = dims[i];
     }
+    // skip layers: hidden layers 1 .. n-2 whose input is [previous output ; posenc]; the posenc
+    // block sits at column Mp[l-1] of the layer's padded input, so the previous width must be a
+    // multiple of 32 (true column k -> padded column k, the padding after them)
+    if (skip_mask >> n_layers) {
+        delete n;
+        return fail(MARF_ERR_INVALID, "net_create: skip mask 0x%x names layers beyond %d", skip_mask, n_layers - 1);
+    }
+    n->skip = skip_mask;
+    for (int l = 0; l < n_layers; ++l) {
+        const bool sk = (skip_mask >> l) & 1u;
+        if (sk && (l == 0 || l == n_layers - 1)) {
+            delete n;
+            return fail(MARF_ERR_UNSUPPORTED, "net_create: skip connection into layer %d (hidden layers 1..%d only)", l,
+                        n_layers - 2);
+        }
+        if (sk && dims[l] % 32) {
+            delete n;
+            return fail(MARF_ERR_UNSUPPORTED, "net_create: skip layer %d needs an input width multiple of 32 (got %d)", l,
+                        dims[l]);
+        }
+        n->kin[l] = dims[l] + (sk ? D : 0);
+    }
     n->Kp[0] = (int)rup(D, 32);
     int hmax = 0;
     for (int l = 0; l < n_layers - 1; ++l) {
         n->Mp[l] = (int)rup(dims[l + 1], 32);
         n->Mt[l] = n->Mp[l];
-        n->Kp[l + 1] = n->Mp[l];
+        n->Kp[l + 1] = n->Mp[l] + (((skip_mask >> (l + 1)) & 1u) ? n->Kp[0] : 0);
         hmax = std::max(hmax, n->Mp[l]);
     }
     n->Mp[n_layers - 1] = 16;
@@ -392,14 +421,16 @@ int marf_net_create_hint(int n_layers, const int* dims, int L, int dtype, long l
     for (int l = 0; l < n_layers; ++l) n->Kmax = std::max(n->Kmax, n->Kp[l]);
     if (hmax > 512 || n->Kmax > 512) {
         delete n;
-        return fail(MARF_ERR_UNSUPPORTED, "net_create: hidden width %d > 512", hmax);
+        return fail(MARF_ERR_UNSUPPORTED, "net_create: hidden width %d / layer input %d > 512", hmax, n->Kmax);
     }
     n->TP = (n->kdt != 0 && n->Kmax <= 256) ? 128 : 64;
     n->lda = n->kdt != 0 ? n->Kmax + 8 : n->Kmax + 1;
     size_t act = (size_t)n->TP * n->lda * n->elem;
     size_t df = (size_t)n->TP * (n->Kp[0] + 1) * 4;
+    // skip nets: the posenc gradient of the skip layers, accumulated beside the tile (fp32 [TP][Kp0])
+    const size_t dsk = n->skip ? (size_t)n->TP * n->Kp[0] * 4 : 0;
     n->lds_fwd = act;
-    n->lds_bwd = std::max(act, df);
+    n->lds_bwd = std::max(act, df) + dsk;
     n->lds_step = n->lds_bwd;
     // The fused step of a 16-bit net wider than 256: one 512-thread block per CU at TP = 128
     // (MARF_STEP_NW=4 at net creation keeps two 4-wave blocks at TP = 64, for A/B runs)
@@ -409,10 +440,11 @@ int marf_net_create_hint(int n_layers, const int* dims, int L, int dtype, long l
         const char* e = getenv("MARF_STEP_NW");
         const bool nw8 = !(e && e[0] == '4');
         const size_t act8 = (size_t)128 * n->lda * n->elem, df8 = (size_t)128 * (n->Kp[0] + 1) * 4;
-        if (nw8 && n->kdt != 0 && n->Kmax > 256 && std::max(act8, df8) + 16 * 1024 <= 160 * 1024) {
+        const size_t dsk8 = n->skip ? (size_t)128 * n->Kp[0] * 4 : 0;
+        if (nw8 && n->kdt != 0 && n->Kmax > 256 && std::max(act8, df8) + dsk8 + 16 * 1024 <= 160 * 1024) {
             n->sTP = 128;
             n->sNW = 8;
-            n->lds_step = std::max(act8, df8);
+            n->lds_step = std::max(act8, df8) + dsk8;
         }
     }
     if (n->lds_bwd > 160 * 1024) {
@@ -423,7 +455,7 @@ int marf_net_create_hint(int n_layers, const int* dims, int L, int dtype, long l
     size_t boff = 0;
     for (int l = 0; l < n_layers; ++l) {
         n->w_off[l] = off;
-        off += (long long)dims[l + 1] * dims[l];
+        off += (long long)dims[l + 1] * n->kin[l];
         n->b_off[l] = off;
         off += dims[l + 1];
         n->wf_off[l] = (long long)boff;
@@ -449,7 +481,7 @@ int marf_net_create_hint(int n_layers, const int* dims, int L, int dtype, long l
     if (dtype == MARF_BF16X3 && n->s2.variant < 0) {
         delete n;
         return fail(MARF_ERR_UNSUPPORTED,
-                    "net_create: split-bf16 needs <= 5 layers, hidden widths <= 256 and L <= 32");
+                    "net_create: split-bf16 needs <= 5 layers, hidden widths <= 256, L <= 32 and no skip layers");
     }
     *out = n;
     return MARF_OK;
@@ -473,7 +505,7 @@ int marf_net_layer_count(const marf_net* net) { return net ? net->n_layers : 0; 
 int marf_net_layer_span(const marf_net* net, int l, long long* off, long long* len) {
     if (!net || l < 0 || l >= net->n_layers || !off || !len) return fail(MARF_ERR_INVALID, "net_layer_span: bad arguments");
     *off = net->w_off[l];
-    *len = (long long)net->dims[l + 1] * net->dims[l] + net->dims[l + 1];  // W_l then b_l
+    *len = (long long)net->dims[l + 1] * net->kin[l] + net->dims[l + 1];  // W_l then b_l
     return MARF_OK;
 }
 const char* marf_net_step_kernel(const marf_net* net) {
@@ -491,7 +523,7 @@ int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, vo
     for (int l = 0; l < net->n_layers; ++l) {
         PackLayer& p = a.ly[l];
         p.M = net->dims[l + 1];
-        p.K = net->dims[l];
+        p.K = net->kin[l];
         p.Mp = net->Mp[l];
         p.Kp = net->Kp[l];
         p.Mt = net->Mt[l];
@@ -551,6 +583,7 @@ static void fill_netdev(const marf_net* n, const void* packed, NetDev& d) {
         d.bias[l] = (const float*)((const char*)packed + n->bias_off[l]);
         d.diag[l] = n->diag[l];
     }
+    d.skip = n->skip;
 }
 
 // ------------------------------------------------------------------ buffer plans
@@ -718,7 +751,7 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
             {
                 MarfProfScope ps("wgrad_reduce", s);
                 HIPCHK(marf_launch_wgrad_reduce(part, bpart, wp.n_chunks, net->Mp[l], net->Kp[l], net->dims[l + 1],
-                                                net->dims[l], d_dparams + net->w_off[l], d_dparams + net->b_off[l], s),
+                                                net->kin[l], d_dparams + net->w_off[l], d_dparams + net->b_off[l], s),
                        "backward wgrad reduce");
             }
         }
@@ -1435,7 +1468,7 @@ int marf_step_backward_ev(const marf_net* net, const marf_geometry* geo, const v
             {
                 MarfProfScope ps("wgrad_reduce", s);
                 HIPCHK(marf_launch_wgrad_reduce(part, bpart, p.n_chunks, net->Mp[l], net->Kp[l], net->dims[l + 1],
-                                                net->dims[l], d_dparams + net->w_off[l], d_dparams + net->b_off[l], s,
+                                                net->kin[l], d_dparams + net->w_off[l], d_dparams + net->b_off[l], s,
                                                 d_gout, denom),
                        "step_backward wgrad reduce");
             }

@@ -185,6 +185,8 @@ struct NetDev {
     const void* Wt[MARF_MAX_LAYERS];  // packed transposed weights (T)
     const float* bias[MARF_MAX_LAYERS];  // padded fp32 bias [Mp]
     unsigned diag[MARF_MAX_LAYERS];      // numerics-experiment rounding codes (MARF_DIAG_RT builds)
+    unsigned skip;                       // bit l: layer l's input is [layer l-1 output ; posenc] (Kp[l] =
+                                         // Mp[l-1] + Kp[0], the posenc block at column Mp[l-1])
 };
 
 // Geometry of the pixel source.

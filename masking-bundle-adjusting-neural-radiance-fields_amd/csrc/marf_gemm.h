@@ -317,16 +317,17 @@ MARF_DEV void c2f_weights_lds(const C2fDev& c2f, int L, float* wsh) {
 // (warp.py:33-81, model/planar.py:451-471; feature layout [u, v, sin_k(u), cos_k(u), sin_k(v),
 // cos_k(v)], zero padded to Kp0).  NPART = 64 NW / TP threads share a pixel: half of them take u,
 // half v, each a contiguous run of bands, written as bf16 pairs (one 4-byte LDS store per pair).
+// c0: the first column (a skip layer's posenc block, written again at column Mp[l-1]; even).
 template <class P, int TP, bool GRID_ONLY = false, int NW = 4>
 MARF_DEV void tile_prologue(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh,
-                            typename P::T* act, int lda, int b, int p0) {
+                            typename P::T* act, int lda, int b, int p0, int c0 = 0) {
     typedef typename P::T T;
     constexpr int NPART = 64 * NW / TP, HALF = NPART / 2;
     const int L = net.L;
     const int i = threadIdx.x % TP, part = threadIdx.x / TP;
     float x, y, u = 0.f, v = 0.f, X[3];
     slot_point<GRID_ONLY>(geo, b, p0 + i, x, y, u, v, X);
-    T* row = act + (size_t)i * lda;
+    T* row = act + (size_t)i * lda + c0;
     auto put2 = [&](int col, float a0, float a1) {  // col even
         if constexpr (sizeof(T) == 2) {
             *reinterpret_cast<uint32_t*>(row + col) = P::pk2(a0, a1);
@@ -469,14 +470,58 @@ MARF_DEV void mask_epilogue(f32x16 (&acc)[RT][PT], typename P::T* act, int lda, 
     }
 }
 
+// Skip layer's dgrad rows past its feature input (rows rt_lo * 32 .. n_rt * 32 = the posenc block,
+// model/planar.py:440-441): no ReLU, the gradient of the posenc features, added into the fp32
+// accumulator dsk [TP][Kp0] (one (pixel, feature) per lane and register: no two lanes share one).
+template <class P, int RT, int PT, int NW = 4>
+MARF_DEV void skip_epilogue(const f32x16 (&acc)[RT][PT], float* dsk, int kp0, int rt_lo, int n_rt, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+        const int rt = wave + NW * i;
+        if (rt < rt_lo || rt >= n_rt) continue;
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const int px = j * 32 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int f = (rt - rt_lo) * 32 + acc_row(lane, r);
+                dsk[(size_t)px * kp0 + f] += acc[i][j][r];
+            }
+        }
+    }
+}
+
+// LDS byte offset of the skip accumulator dsk: past the activation tile and the fp32 df image
+template <class P, int TP>
+MARF_DEV int skip_lds_off(const NetDev& net, int lda) {
+    const int a = TP * lda * (int)sizeof(typename P::T), d = TP * (net.Kp[0] + 1) * 4;
+    return ((a > d ? a : d) + 15) & ~15;
+}
+
+// One dgrad layer of the tile kernels: dz_l = (W_l^T dz_{l+1}) * relu'(feat_l) into act (the ReLU
+// record of feat_l), and for a skip layer the posenc rows into dsk.  acc holds the GEMM.
+template <class P, int RT, int PT, int NW = 4>
+MARF_DEV void dgrad_epilogue(f32x16 (&acc)[RT][PT], const NetDev& net, int l, typename P::T* act, int lda, int wave,
+                             int lane, uint4 mw, float* dsk) {
+    const int R = net.Kp[l];
+    if ((net.skip >> l) & 1u) {
+        mask_epilogue<P, RT, PT, NW>(acc, act, lda, net.Mp[l - 1] / 32, wave, lane, mw, net.diag[l - 1]);
+        skip_epilogue<P, RT, PT, NW>(acc, dsk, net.Kp[0], net.Mp[l - 1] / 32, R / 32, wave, lane);
+    } else {
+        mask_epilogue<P, RT, PT, NW>(acc, act, lda, R / 32, wave, lane, mw, net.diag[l - 1]);
+    }
+}
+
 // Layer-0 dgrad (d feat_0 = W_0^T dz_1, act holds dz_1) and the posenc / projective-warp adjoint
 // (model/planar.py:451-471, warp.py:74-78 backward): per slot d(u, v), then for the grid geometry
 // d(Hx) and one dH[3x3] partial per tile (fixed-order wave + block sums); for explicit coordinates
 // d coords.  `red` needs 64 NW * 2 floats, `red9` NW * 9.  smem = the act tile (reused as fp32).
+// dsk: the skip layers' posenc gradient ([TP][Kp0] fp32, added to d feat_0), or null.
 template <class P, int TP, bool GRID_ONLY = false, int NW = 4>
 MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, const float* wsh, char* smem, int lda,
                            int wave, int lane, int b, int p0, float* red, float* red9, float* dH_partial,
-                           float* d_coords, TileStore<typename P::T>& st, unsigned long long* sp = nullptr) {
+                           float* d_coords, TileStore<typename P::T>& st, unsigned long long* sp = nullptr,
+                           const float* dsk = nullptr) {
     typedef typename P::T T;
     constexpr int PT = TP / 32;
     constexpr int RT = 8 / PT;
@@ -501,6 +546,13 @@ MARF_DEV void warp_adjoint(const NetDev& net, const GeoDev& geo, int c2f_on, con
         }
     }
     __syncthreads();
+    if (dsk) {  // points_enc feeds layer 0 and every skip layer: its gradient is their sum
+        for (int e = threadIdx.x; e < TP * R; e += 64 * NW) {
+            const int px = e / R, c = e - px * R;
+            df[(size_t)px * ldf + c] += dsk[e];
+        }
+        __syncthreads();
+    }
     MARF_STAMP(sp, 17);
 
     // posenc adjoint: d coord_c = df[c] + sum_k w_k f_k (cos(x_k) df_sin - sin(x_k) df_cos)

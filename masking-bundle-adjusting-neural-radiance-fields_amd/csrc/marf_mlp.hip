@@ -58,10 +58,15 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
         __syncthreads();  // every wave has consumed the layer input
         relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask[l + 1], blockIdx.x, net.diag[l + 1]);
         __syncthreads();
+        if ((net.skip >> (l + 1)) & 1u) {  // skip layer: [feature ; posenc] (model/planar.py:440-441)
+            tile_prologue<P, TP>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0, M);
+            __syncthreads();
+        }
         st.clear();
         if (a.feat[l + 1]) {
+            const int Kn = net.Kp[l + 1];  // (M + Kp0 for a skip layer)
             if (l + 1 < nl - 1)
-                save_tile<P>(st, act, lda, TP, M, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M / P::KS);
+                save_tile<P>(st, act, lda, TP, Kn, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * Kn, Kn / P::KS);
             else  // input of the last (16x16) layer: plain copy
                 copy_tile_out<P>(act, lda, TP, M, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M);
         }
@@ -126,6 +131,11 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(BwdArgs a) {
     const int nl = net.n_layers;
 
     c2f_weights_lds(a.c2f, net.L, wsh);
+    float* dsk = nullptr;  // skip nets: the posenc gradient of the skip layers
+    if (net.skip) {
+        dsk = reinterpret_cast<float*>(smem + skip_lds_off<P, TP>(net, lda));
+        for (int e = threadIdx.x; e < TP * net.Kp[0]; e += 256) dsk[e] = 0.f;
+    }
 
     // ---- sigmoid backward: g = d_rgb * (1 - y) * y   (torch sigmoid_backward)
     if ((int)threadIdx.x < TP) {
@@ -155,13 +165,14 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(BwdArgs a) {
         const uint4 mw = *mask_record(const_cast<uint64_t*>(a.mask[l]), blockIdx.x, wave, lane);
         gemm_tile<P, RT, PT>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
         __syncthreads();
-        mask_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, mw, net.diag[l - 1]);
+        dgrad_epilogue<P, RT, PT>(acc, net, l, act, lda, wave, lane, mw, dsk);
         __syncthreads();
         save_tile<P>(st, act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, net.Mt[l - 1] / P::KS);
     }
 
     // ---- layer 0 dgrad + posenc / warp adjoint
-    warp_adjoint<P, TP>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, a.d_coords, st);
+    warp_adjoint<P, TP>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, a.d_coords, st,
+                        nullptr, dsk);
 }
 
 }  // namespace marf

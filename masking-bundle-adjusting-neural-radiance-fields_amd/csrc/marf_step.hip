@@ -118,10 +118,16 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
         relu_epilogue<P, RT, PT, NW>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x, net.diag[l + 1]);
         __syncthreads();
         if (l < 3) STAMP(3 + 2 * l);
+        if ((net.skip >> (l + 1)) & 1u) {  // skip layer: [feature ; posenc] (model/planar.py:440-441)
+            tile_prologue<P, TP, true, NW>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0, M);
+            __syncthreads();
+        }
         st.clear();
-        if (l + 1 < nl - 1)  // the last layer's input never leaves LDS
-            save_tile<P, NW>(st, act, lda, TP, M, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * M, M / P::KS,
-                            MARF_DIAG_SAVE(net));
+        if (l + 1 < nl - 1) {  // the last layer's input never leaves LDS
+            const int Kn = net.Kp[l + 1];  // (M + Kp0 for a skip layer)
+            save_tile<P, NW>(st, act, lda, TP, Kn, reinterpret_cast<T*>(a.feat[l + 1]) + slot0 * Kn, Kn / P::KS,
+                             MARF_DIAG_SAVE(net));
+        }
     };
     for (int l = 0; l < nl - 2; ++l) hidden(l);
     constexpr int NWL = 8;  // prefetched last-layer k-steps (16x16 fragments)
@@ -294,13 +300,18 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
 
     // ---- dgrad chain, l = n-1 .. 1 : dfeat_l = W_l^T dz_{l+1}; dz_l = dfeat_l * relu'(feat_l)
     st.clear();
+    float* dsk = nullptr;  // skip nets: the posenc gradient of the skip layers
+    if (net.skip) {
+        dsk = reinterpret_cast<float*>(smem + skip_lds_off<P, TP>(net, lda));
+        for (int e = threadIdx.x; e < TP * net.Kp[0]; e += 64 * NW) dsk[e] = 0.f;
+    }
     for (int l = nl - 1; l >= 1; --l) {
         const int R = net.Kp[l], Kk = net.Mt[l], n_rt = R / 32;
         f32x16 acc[RT][PT];
         const uint4 mw = *mask_record(a.mask_bits[l], blockIdx.x, wave, lane, NW);  // in flight behind the GEMM
         gemm_tile<P, RT, PT, NW>(acc, reinterpret_cast<const T*>(net.Wt[l]), Kk, n_rt, act, lda, wave, lane, nullptr, st);
         __syncthreads();
-        mask_epilogue<P, RT, PT, NW>(acc, act, lda, n_rt, wave, lane, mw, net.diag[l - 1]);
+        dgrad_epilogue<P, RT, PT, NW>(acc, net, l, act, lda, wave, lane, mw, dsk);
         __syncthreads();
         if (l <= 4) STAMP(15 - l);  // 14 .. 11
         save_tile<P, NW>(st, act, lda, TP, R, reinterpret_cast<T*>(a.dz[l]) + slot0 * R, net.Mt[l - 1] / P::KS,
@@ -309,9 +320,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
 
     // ---- layer-0 dgrad + posenc / warp adjoint -> dH partial
 #ifdef MARF_STAMPS
-    warp_adjoint<P, TP, true, NW>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st, sp);
+    warp_adjoint<P, TP, true, NW>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st, sp,
+                                  dsk);
 #else
-    warp_adjoint<P, TP, true, NW>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st);
+    warp_adjoint<P, TP, true, NW>(net, a.geo, a.c2f.on, wsh, smem, lda, wave, lane, b, p0, red, red9, a.dH_partial, nullptr, st,
+                                  nullptr, dsk);
 #endif
     STAMP(15);
 }

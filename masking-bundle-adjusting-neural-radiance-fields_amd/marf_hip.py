@@ -46,6 +46,8 @@ _SIGS = {
                                      _c_vp]),
     "marf_net_create": (_c_int, [_c_int, ctypes.POINTER(_c_int), _c_int, _c_int, ctypes.POINTER(_c_vp)]),
     "marf_net_create_hint": (_c_int, [_c_int, ctypes.POINTER(_c_int), _c_int, _c_int, _c_ll, ctypes.POINTER(_c_vp)]),
+    "marf_net_create_skip": (_c_int, [_c_int, ctypes.POINTER(_c_int), _c_int, _c_int, _c_ll, ctypes.c_uint,
+                                      ctypes.POINTER(_c_vp)]),
     "marf_net_destroy": (None, [_c_vp]),
     "marf_net_param_count": (_c_ll, [_c_vp]),
     "marf_net_packed_bytes": (_c_sz, [_c_vp]),
@@ -372,15 +374,22 @@ def posenc(coord, L, progress=None, c2f=None):
 # ====================================================================== MLP engine
 
 class Net:
-    """An MLP shape + padding plan in the library (marf_net)."""
+    """An MLP shape + padding plan in the library (marf_net).  skip: the layer indices whose input
+    is [previous output ; posenc features] (opt.arch.skip, model/planar.py:419-420, 440-441)."""
 
-    def __init__(self, dims, L, dtype, pixels_hint=0):
+    def __init__(self, dims, L, dtype, pixels_hint=0, skip=()):
         self.dims = [int(d) for d in dims]
         self.L = int(L)
         self.dtype = dtype
+        self.skip = sorted(int(s) for s in skip)
+        mask = 0
+        for s_ in self.skip:
+            if not 0 <= s_ < 32:
+                raise ValueError(f"skip layer {s_}")
+            mask |= 1 << s_
         arr = (_c_int * len(self.dims))(*self.dims)
         h = _c_vp()
-        _check(lib().marf_net_create_hint(len(self.dims) - 1, arr, self.L, dtype, int(pixels_hint), ctypes.byref(h)))
+        _check(lib().marf_net_create_skip(len(self.dims) - 1, arr, self.L, dtype, int(pixels_hint), mask, ctypes.byref(h)))
         self._h = h
         self.param_count = lib().marf_net_param_count(h)
         self.packed_bytes = lib().marf_net_packed_bytes(h)
@@ -679,8 +688,8 @@ def geo_np(engine):
 class Engine:
     """Library-side state of one NeuralImageFunction: net plan, packed weights, c2f, geometry."""
 
-    def __init__(self, dims, L, dtype, c2f, H, W, patch_H, patch_W, lie_batch=0, crop=True, pixels_hint=0):
-        self.net = Net(dims, L, dtype, pixels_hint)
+    def __init__(self, dims, L, dtype, c2f, H, W, patch_H, patch_W, lie_batch=0, crop=True, pixels_hint=0, skip=()):
+        self.net = Net(dims, L, dtype, pixels_hint, skip)
         self.c2f = c2f
         self.H, self.W, self.patch_H, self.patch_W = H, W, patch_H, patch_W
         self.crop = bool(crop)

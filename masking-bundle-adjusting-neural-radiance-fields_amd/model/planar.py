@@ -545,15 +545,20 @@ class NeuralImageFunction(torch.nn.Module):
     def input_dim(self):
         return 2 + 4 * self.L if self.opt.arch.posenc else 2
 
+    @property
+    def skip(self):
+        return [int(s) for s in (self.opt.arch.skip or [])]
+
     def define_network(self):
         """Linear layers in module order (this order is the RNG order of the init), layer 0
-        rescaled by sqrt(D_in / 2) when coarse-to-fine is on."""
-        if self.opt.arch.skip:
-            raise NotImplementedError("skip connections are not used by the planar model")
+        rescaled by sqrt(D_in / 2) when coarse-to-fine is on; a skip layer takes the posenc
+        features beside its input (k_in + D, model/planar.py:419-420)."""
         widths = list(self.opt.arch.layers)
         widths[0] = self.input_dim
         self.mlp = torch.nn.ModuleList()
         for li, (k_in, k_out) in enumerate(util.get_layer_dims(widths)):
+            if li in self.skip:
+                k_in += self.input_dim
             layer = torch.nn.Linear(k_in, k_out)
             if self.opt.barf_c2f and li == 0:
                 s = np.sqrt(self.input_dim / 2.)
@@ -587,7 +592,7 @@ class NeuralImageFunction(torch.nn.Module):
             hint = -(-int(o.batch_size) // world) * ph * pw
             e = marf_hip.Engine(dims, self.L, _precision(o), list(o.barf_c2f) if o.barf_c2f else None,
                                 o.H, o.W, ph, pw, lie_batch=int(o.batch_size), crop=bool(o.use_cropped_images),
-                                pixels_hint=hint)
+                                pixels_hint=hint, skip=self.skip)
             self._engines[key] = e
         return e
 

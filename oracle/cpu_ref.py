@@ -102,11 +102,15 @@ class CpuRefStep:
 
     def render(self, coord):
         L = self.cfg["L"]
-        feat = coord
+        points_enc = coord
         if L > 0:
             enc = positional_encoding(coord, L, self.progress.data, self.cfg["c2f"])
-            feat = torch.cat([coord, enc], -1)
+            points_enc = torch.cat([coord, enc], -1)
+        feat = points_enc
+        skip = self.cfg.get("skip", ())
         for li, lin in enumerate(self.mlp):
+            if li in skip:  # model/planar.py:440-441
+                feat = torch.cat([feat, points_enc], -1)
             feat = lin(feat)
             if li != len(self.mlp) - 1:
                 feat = torch.relu(feat)

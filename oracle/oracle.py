@@ -146,36 +146,49 @@ def prologue_backward(xy, Hm, dfeat, L, w, want_dH=True):
 
 # ------------------------------------------------------------------------ MLP
 
-def mlp_forward(f0, params):
-    """NeuralImageFunction.forward MLP part, model/planar.py:437-448 (skip=[]).
-    params: [(W [out,in], b [out]), ...] fp32.  Returns (acts, rgb) with
-    acts[l] the input of layer l (acts[0] = f0, acts[l>0] post-ReLU)."""
-    acts = [np.asarray(f0, np.float32)]
-    x = acts[0]
+def mlp_forward(f0, params, skip=()):
+    """NeuralImageFunction.forward MLP part, model/planar.py:437-448; a layer li in `skip` takes
+    cat([feat, points_enc]) (:440-441).  params: [(W [out,in], b [out]), ...] fp32.  Returns (acts,
+    rgb) with acts[l] the input of layer l (acts[0] = f0, acts[l>0] post-ReLU, concatenated with f0
+    for a skip layer)."""
+    f0 = np.asarray(f0, np.float32)
+    acts = []
+    x = f0
     n = len(params)
     for li, (W, b) in enumerate(params):
+        if li in skip:
+            x = np.concatenate([x, f0], axis=-1)
+        acts.append(x)
         z = x @ W.T + b
         if li != n - 1:
             x = np.maximum(z, np.float32(0))
-            acts.append(x)
         else:
             x = np.float32(1) / (np.float32(1) + np.exp(-z))
     return acts, x.astype(np.float32)
 
 
-def mlp_backward(acts, rgb, d_rgb, params):
-    """Autograd of mlp_forward: returns ([(dW, db)], d_f0)."""
+def mlp_backward(acts, rgb, d_rgb, params, skip=()):
+    """Autograd of mlp_forward: returns ([(dW, db)], d_f0); a skip layer's input gradient splits into
+    the previous layer's (ReLU-masked) and the posenc features', which autograd adds to layer 0's."""
     g = (d_rgb * (np.float32(1) - rgb) * rgb).astype(np.float32)
     grads = [None] * len(params)
+    d_enc = None
+    D = acts[0].shape[-1]
     for li in range(len(params) - 1, -1, -1):
         W, _ = params[li]
         a = acts[li]
         grads[li] = ((g.T @ a).astype(np.float32), g.sum(0, dtype=np.float64).astype(np.float32))
-        d = g @ W
+        d = (g @ W).astype(np.float32)
+        if li in skip:
+            de = d[:, -D:]
+            d_enc = de if d_enc is None else (d_enc + de).astype(np.float32)
+            d, a = d[:, :-D], a[:, :-D]
         if li > 0:
             g = (d * (a > 0)).astype(np.float32)
         else:
-            g = d.astype(np.float32)
+            g = d
+    if d_enc is not None:
+        g = (d_enc + g).astype(np.float32)
     return grads, g
 
 
@@ -260,7 +273,7 @@ class PlanarStep:
         uv = warp_points(xyB, Hm)
         w = c2f_weights(self.progress, cfg["c2f"], L)
         f0 = posenc_features(uv, L, w).reshape(-1, 2 + 4 * L)
-        acts, rgb = mlp_forward(f0, self.params)
+        acts, rgb = mlp_forward(f0, self.params, cfg.get("skip", ()))
         return dict(Hm=Hm, xyB=xyB, uv=uv, w=w, acts=acts, rgb=rgb)
 
     def alpha(self):
@@ -281,7 +294,7 @@ class PlanarStep:
         gout = np.float32(np.float32(1 - alpha) + np.float32(1.0))
         dpred = masked_mse_backward(pred, self.rgb, self.mask, denom, gout)
         d_rgb = dpred.transpose(0, 2, 3, 1).reshape(-1, 3)
-        grads, df0 = mlp_backward(fw["acts"], fw["rgb"], d_rgb, self.params)
+        grads, df0 = mlp_backward(fw["acts"], fw["rgb"], d_rgb, self.params, cfg.get("skip", ()))
         L = cfg["L"]
         dH, _ = prologue_backward(fw["xyB"], fw["Hm"], df0.reshape(B, -1, 2 + 4 * L), L, fw["w"])
         dh = sl3_to_SL3_backward(self.warp, dH.astype(np.float32))

@@ -187,6 +187,45 @@ def make_step_small():
     np.savez_compressed(os.path.join(HERE, "step_small.npz"), **out)
 
 
+def make_step_skip():
+    """arch.skip (model/planar.py:419-420, 440-441): the reference's Graph with skip layers, 6 steps,
+    the same fields as step_small."""
+    out = {}
+    cases = {
+        # tag: (overrides, progress)
+        "s1": ({"arch": {"layers": [None, 64, 64, 64, 3], "skip": [2], "posenc": {"L_2D": 8}}, "barf_c2f": [0, 0.4]},
+               0.3),
+        "s2": ({"arch": {"layers": [None, 64, 64, 64, 64, 3], "skip": [1, 3], "posenc": {"L_2D": 4}}, "barf_c2f": None,
+                "use_edges": False}, None),
+    }
+    rng = np.random.default_rng(17)
+    for tag, (over, prog) in cases.items():
+        geo = {"H": 36, "W": 48, "patch_H": 18, "patch_W": 24, "batch_size": 3, "max_iter": 50}
+        geo.update(over)
+        opt = R.make_opt(geo)
+        rgb, mask = synth_images(3, 18, 24, seed=200 + ord(tag[1]))
+        warp0 = rng.normal(0, 0.03, (3, 8)).astype(np.float32)
+        res = ref_train(opt, rgb, mask, warp_init=warp0, progress=prog, steps=6)
+        L = opt.arch.posenc.L_2D if opt.arch.posenc else 0
+        c2f = opt.barf_c2f
+        out[f"{tag}_cfg"] = np.array([36, 48, 18, 24, 3, L, -1 if c2f is None else c2f[0],
+                                      -1 if c2f is None else c2f[1], 50,
+                                      -1 if prog is None else prog, 1 if opt.use_edges else 0], np.float64)
+        out[f"{tag}_layers"] = np.array([2 + 4 * L] + list(opt.arch.layers[1:]), np.int64)
+        out[f"{tag}_skip"] = np.array(opt.arch.skip, np.int64)
+        out[f"{tag}_rgb"], out[f"{tag}_mask"], out[f"{tag}_warp0"] = rgb, mask, warp0
+        for k, v in res["init"].items():
+            out[f"{tag}_init_{k}"] = v
+        for k, v in res["grads0"].items():
+            out[f"{tag}_grad0_{k}"] = v
+        for k, v in res["final"].items():
+            out[f"{tag}_final_{k}"] = v
+        out[f"{tag}_rgb0"] = res["rgb0"]
+        out[f"{tag}_loss"] = np.array(res["loss"], np.float64)
+        out[f"{tag}_warp_traj"] = np.stack(res["warp"])
+    np.savez_compressed(os.path.join(HERE, "step_skip.npz"), **out)
+
+
 def load_cat_batch3(opt):
     D = os.path.join(R.REF, "data", "planar", opt.dataset)
     rgb = R.load_images_pil([f"{D}/{i}.png" for i in range(opt.batch_size)], opt)
@@ -314,6 +353,8 @@ if __name__ == "__main__":
         make_api()
     if "c1L10" in which:
         make_step_c1_L10()
+    if "skip" in which:
+        make_step_skip()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -65,6 +65,31 @@ def test_net_create_rejects_bad_shapes(lib):
         marf_hip.Net([34, 1024, 3], 8, marf_hip.MARF_BF16)
 
 
+def test_skip_net_planning(lib):
+    """marf_net_create_skip (opt.arch.skip, model/planar.py:419-420): a skip layer's weight is
+    [out, in + 2+4L] in the flat parameter vector (torch's nn.Linear shapes, in layer order);
+    skip into layer 0 or the output layer, a non-multiple-of-32 previous width and the split-bf16
+    recipe are refused."""
+    import marf_hip
+    n = marf_hip.Net([34, 64, 64, 64, 3], 8, marf_hip.MARF_FP32, skip=[2])
+    assert n.param_count == (34 * 64 + 64) + (64 * 64 + 64) + ((64 + 34) * 64 + 64) + (64 * 3 + 3)
+    assert [s for _, s in n.layer_spans] == [35 * 64, 65 * 64, 99 * 64, 65 * 3]  # W_l then b_l
+    assert n.step_kernel != "step2"
+    for dt in (marf_hip.MARF_BF16, marf_hip.MARF_FP16):
+        assert marf_hip.Net([18, 64, 64, 64, 64, 3], 4, dt, skip=[1, 3]).param_count == \
+            (18 * 64 + 64) + (82 * 64 + 64) + (64 * 64 + 64) + (82 * 64 + 64) + (64 * 3 + 3)
+    with pytest.raises(RuntimeError, match="skip connection"):
+        marf_hip.Net([34, 64, 64, 3], 8, marf_hip.MARF_FP32, skip=[0])
+    with pytest.raises(RuntimeError, match="skip connection"):
+        marf_hip.Net([34, 64, 64, 3], 8, marf_hip.MARF_FP32, skip=[2])
+    with pytest.raises(RuntimeError, match="multiple of 32"):
+        marf_hip.Net([34, 60, 64, 3], 8, marf_hip.MARF_FP32, skip=[1])
+    with pytest.raises(RuntimeError, match="skip"):
+        marf_hip.Net([66, 256, 256, 256, 256, 3], 16, marf_hip.MARF_BF16X3, skip=[2])
+    with pytest.raises(RuntimeError, match="512"):
+        marf_hip.Net([66, 512, 512, 512, 3], 16, marf_hip.MARF_BF16, skip=[2])  # 512 + 96 inputs
+
+
 def test_product_refuses_cpu_tensors(lib):
     import torch
     import marf_hip

@@ -14,16 +14,18 @@ def _case(g, tag):
               for i in range(len(layers) - 1)]
     c = dict(H=int(H), W=int(W), patch_H=int(ph), patch_W=int(pw), L=int(L), c2f=None if c0 < 0 else [c0, c1],
              max_iter=int(max_iter), lr=1e-3, lr_warp=1e-3, fix_first=True, use_edges=bool(use_edges),
-             alpha_initial=0.0, alpha_final=1.0)
+             alpha_initial=0.0, alpha_final=1.0,
+             skip=tuple(int(x) for x in g[f"{tag}_skip"]) if f"{tag}_skip" in g.files else ())
     st = cpu_ref.CpuRefStep(c, params, g[f"{tag}_warp0"], g[f"{tag}_rgb"], g[f"{tag}_mask"])
     if prog >= 0:
         st.progress.data.fill_(float(prog))
     return st, len(layers) - 1
 
 
-@pytest.mark.parametrize("tag", ["a", "b", "c", "d"])
-def test_small_step_vs_reference(golden, tag):
-    g = golden("step_small")
+@pytest.mark.parametrize("fix,tag", [("step_small", "a"), ("step_small", "b"), ("step_small", "c"),
+                                     ("step_small", "d"), ("step_skip", "s1"), ("step_skip", "s2")])
+def test_small_step_vs_reference(golden, fix, tag):
+    g = golden(fix)
     st, nl = _case(g, tag)
     r = st.step()
     np.testing.assert_allclose(r["rgb"].reshape(g[f"{tag}_rgb0"].shape), g[f"{tag}_rgb0"], atol=1e-6, rtol=0)

@@ -120,18 +120,19 @@ def test_posenc_c2f(tag):
 
 # ------------------------------------------------------------------------ full step, small
 
-SMALL = ("a", "b", "c", "d")
+SMALL = ("a", "b", "c", "d", "s1", "s2")  # s1, s2: arch.skip nets (tests/golden/step_skip.npz)
 
 
 def small_setup(tag, precision="fp32", tmp_path=None):
     from model import planar
     from util import EasyDict as edict
-    z = g("step_small")
+    z = g("step_skip" if tag.startswith("s") else "step_small")
     H, W, ph, pw, B, L, c0, c1, max_iter, prog, use_edges = z[f"{tag}_cfg"]
     layers = [None] + [int(x) for x in z[f"{tag}_layers"][1:]]
+    skip = [int(x) for x in z[f"{tag}_skip"]] if f"{tag}_skip" in z.files else []
     opt = make_opt(tmp_path, H=int(H), W=int(W), patch_H=int(ph), patch_W=int(pw), batch_size=int(B),
                    max_iter=int(max_iter), use_edges=bool(use_edges), precision=precision,
-                   arch={"layers": layers, "skip": [], "posenc": ({"L_2D": int(L)} if L > 0 else None)},
+                   arch={"layers": layers, "skip": skip, "posenc": ({"L_2D": int(L)} if L > 0 else None)},
                    barf_c2f=None if c0 < 0 else [float(c0), float(c1)])
     m = planar.Model(opt)
     m.images = edict(rgb=t(z[f"{tag}_rgb"]), masks=t(z[f"{tag}_mask"]), masks_eroded=t(z[f"{tag}_mask"]),
@@ -172,7 +173,7 @@ def test_small_step_fp32_vs_reference(tag, tmp_path):
     var, loss = one_step_grads(m, var)
     rgb = var.rgb_prediction.detach().cpu().numpy().reshape(z[f"{tag}_rgb0"].shape)
     np.testing.assert_allclose(rgb, z[f"{tag}_rgb0"], atol=1e-5, rtol=0)  # fp32: 1e-5
-    np.testing.assert_allclose(float(loss.rgb), z[f"{tag}_loss"][0], rtol=1e-5)
+    np.testing.assert_allclose(float(loss.rgb.detach()), z[f"{tag}_loss"][0], rtol=1e-5)
     for i in range(nl):
         for name in ("weight", "bias"):
             got = getattr(m.graph.neural_image.mlp[i], name).grad.cpu().numpy()
@@ -202,7 +203,7 @@ def test_small_trajectory_fp32_vs_reference(tag, tmp_path):
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])
-@pytest.mark.parametrize("tag", ["a", "c"])
+@pytest.mark.parametrize("tag", ["a", "c", "s1"])
 def test_small_step_bf16(tag, precision, tmp_path):
     """Plain 16-bit MFMA recipes (bf16; fp16 = MARF_FP16, 11 significant bits) against the
     reference's first step: rgb 1e-2 abs, loss 2e-2 rel, MLP-gradient cosine > 0.99."""
@@ -216,6 +217,48 @@ def test_small_step_bf16(tag, precision, tmp_path):
         ref = z[f"{tag}_grad0_neural_image.mlp.{i}.weight"].ravel()
         cos = got @ ref / (np.linalg.norm(got) * np.linalg.norm(ref) + 1e-30)
         assert cos > 0.99, (tag, i, cos)
+
+
+def test_skip_net_forward_paths_vs_oracle(tmp_path):
+    """arch.skip nets through the non-fused paths (model/planar.py:429-449 with skip): the
+    explicit-coordinates forward (NeuralImageFunction.forward, k_mlp_fwd) and its autograd
+    (k_mlp_bwd) against the oracle, fp32 1e-5; the unfused training step (opt.fused_step False:
+    marf_forward + marf_backward) against the fused one; the split-bf16 recipe refuses skip nets."""
+    import marf_hip
+    from model import planar
+    z, m, var, nl = small_setup("s1", "fp32", tmp_path)
+    ni = m.graph.neural_image
+    params = [(l.weight.detach().cpu().numpy(), l.bias.detach().cpu().numpy()) for l in ni.mlp]
+    rng = np.random.default_rng(9)
+    coords = (rng.random((1000, 2)) * 2 - 1).astype(np.float32)
+    c = t(coords).requires_grad_()
+    rgb = ni.forward(c)
+    w = oracle.c2f_weights(np.float32(float(ni.progress)), m.opt.barf_c2f, ni.L)
+    f0 = oracle.posenc_features(coords, ni.L, w)
+    acts, ref = oracle.mlp_forward(f0, params, ni.skip)
+    assert np.abs(rgb.detach().cpu().numpy() - ref).max() <= 1e-5
+    d = rng.standard_normal((1000, 3)).astype(np.float32)
+    rgb.backward(t(d))
+    grads, df0 = oracle.mlp_backward(acts, ref, d, params, ni.skip)
+    for i, lay in enumerate(ni.mlp):
+        got, r = lay.weight.grad.cpu().numpy(), grads[i][0]
+        assert np.abs(got - r).max() <= 1e-5 * np.abs(r).max(), i
+    # the coordinate gradient carries the skip layer's posenc share (df0 = layer 0's + skip's)
+    _, duv = oracle.prologue_backward(coords.reshape(1, -1, 2), np.eye(3, dtype=np.float32)[None],
+                                      df0.reshape(1, -1, f0.shape[-1]), ni.L, w, want_dH=False)
+    np.testing.assert_allclose(c.grad.cpu().numpy(), duv.reshape(-1, 2), atol=1e-5 * np.abs(duv).max() + 1e-6)
+    # unfused vs fused training step: the same gradients to fp32 summation order
+    res = {}
+    for fused in (True, False):
+        z, m, var, nl = small_setup("s1", "fp32", tmp_path)
+        m.opt.fused_step = fused
+        var, loss = one_step_grads(m, var)
+        res[fused] = ([l.weight.grad.cpu().numpy() for l in m.graph.neural_image.mlp],
+                      m.graph.warp_param.weight.grad.cpu().numpy())
+    for a, b in zip(res[True][0] + [res[True][1]], res[False][0] + [res[False][1]]):
+        assert np.abs(a - b).max() <= 1e-5 * np.abs(a).max() + 1e-12
+    with pytest.raises(RuntimeError, match="skip"):
+        small_setup("s1", "bf16x3", tmp_path)[1].graph.neural_image.engine(torch.device(DEV))
 
 
 # ------------------------------------------------------------------------ real C1 (cat_batch3)

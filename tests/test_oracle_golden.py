@@ -78,16 +78,20 @@ def _small_case(g, tag):
     params = [(g[f"{tag}_init_neural_image.mlp.{i}.weight"], g[f"{tag}_init_neural_image.mlp.{i}.bias"])
               for i in range(len(layers) - 1)]
     c = dict(H=int(H), W=int(W), patch_H=int(ph), patch_W=int(pw), L=int(L), c2f=c2f, max_iter=int(max_iter),
-             lr=1e-3, lr_warp=1e-3, fix_first=True, use_edges=bool(use_edges), alpha_initial=0.0, alpha_final=1.0)
+             lr=1e-3, lr_warp=1e-3, fix_first=True, use_edges=bool(use_edges), alpha_initial=0.0, alpha_final=1.0,
+             skip=tuple(int(x) for x in g[f"{tag}_skip"]) if f"{tag}_skip" in g.files else ())
     st = oracle.PlanarStep(c, params, g[f"{tag}_warp0"], g[f"{tag}_rgb"], g[f"{tag}_mask"])
     if prog >= 0:
         st.progress = np.float32(prog)
     return st, len(layers) - 1
 
 
-@pytest.mark.parametrize("tag", ["a", "b", "c", "d"])
-def test_small_step_vs_reference(golden, tag):
-    g = golden("step_small")
+@pytest.mark.parametrize("fix,tag", [("step_small", "a"), ("step_small", "b"), ("step_small", "c"),
+                                     ("step_small", "d"), ("step_skip", "s1"), ("step_skip", "s2")])
+def test_small_step_vs_reference(golden, fix, tag):
+    """One step and a 6-step trajectory of the reference's Graph (tests/golden/make_golden.py); the
+    step_skip cases have arch.skip layers (model/planar.py:419-420, 440-441)."""
+    g = golden(fix)
     st, nl = _small_case(g, tag)
     r = st.step()
     np.testing.assert_allclose(r["rgb"].reshape(g[f"{tag}_rgb0"].shape), g[f"{tag}_rgb0"], atol=2e-6, rtol=0)
