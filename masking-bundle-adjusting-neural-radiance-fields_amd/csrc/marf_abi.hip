@@ -1054,7 +1054,7 @@ static int wgrad_piece(const marf_net* net, const GeoDev& g, const Step2BufPlan&
         MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s2);
         if (l == 0 && f0)
             HIPCHK(marf_launch_wgrad_l0_recompute(sv + p.dz[1], net->Kp[1], g, (const float*)(sv + p.c2f), net->L, q.nk0w,
-                                                  p.S, net->Mp[0], 32, r.n, part, bpart, s2, &r),
+                                                  q.ldf0, p.S, net->Mp[0], 32, r.n, part, bpart, s2, &r),
                    "step_forward pipelined wgrad_l0");
         else
             HIPCHK(marf_launch_wgrad(1, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K, 32, r.n,
@@ -1308,7 +1308,7 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                 MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
                 if (l == 0 && f0)
                     HIPCHK(marf_launch_wgrad_l0_recompute(sv + p.dz[1], net->Kp[1], g, (const float*)(sv + p.c2f), net->L,
-                                                          q.nk0w, p.S, net->Mp[0], (int)chunk, n_chunks, part, bpart, s),
+                                                          q.nk0w, q.ldf0, p.S, net->Mp[0], (int)chunk, n_chunks, part, bpart, s),
                            "step_backward wgrad_l0 (feat_0 recomputed)");
                 else
                     HIPCHK(marf_launch_wgrad(1, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K,

@@ -150,7 +150,7 @@ struct WgRange {
 bool marf_wgrad_range_ok(int dtype, int M, int ldz, int K, int ldf);
 bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk, int n_chunks, long long Np_pad);
 hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev& geo, const float* c2f_w, int L,
-                                          int nk0, long long S, int M, int chunk, int n_chunks, float* partial,
+                                          int nk0, int K0, long long S, int M, int chunk, int n_chunks, float* partial,
                                           float* bpartial, hipStream_t s, const WgRange* rng = nullptr);
 hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
                              int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s,

@@ -473,6 +473,7 @@ MARF_DEV void wgrad_dma_body(const WgArgs& a, int chunk_id, int ob, char* smem) 
 #pragma unroll
         for (int j = 0; j < CT; ++j) {
             const int k = (wc * CT + j) * 32 + (lane & 31);
+            if (KF != 256 && k0 + k >= a.K) continue;  // (a 64-wide layer-0 partial from the 96-wide stage)
 #pragma unroll
             for (int r = 0; r < 16; ++r) out[(size_t)((wr * RT + i) * 32 + acc_row(lane, r)) * a.K + k] = acc[i][j][r];
         }
@@ -733,7 +734,7 @@ static bool wgrad_dma_enabled() {
 template <class P, int KF, bool F0 = false>
 static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
     a.n_chunks = n_chunks;
-    a.n_oblk_c = a.K / KF;
+    a.n_oblk_c = (a.K + KF - 1) / KF;
     constexpr int SP = F0 ? WG_SP0 : KF == 256 ? WG_SPH : 32;
     constexpr int NBUF = KF == 256 ? WG_NBUF_H : F0 ? WG_NBUF_0 : WG_NBUF_96;  // ring depth within 160 KB of LDS
     const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024) + (F0 ? (9 * F0_PATCHES + 32 + (NBUF + 1) * SP * 2) * 4 : 0);
@@ -814,14 +815,16 @@ bool marf_wgrad_range_ok(int dtype, int M, int ldz, int K, int ldf) {
 }
 
 // Layer-0 weight gradient with feat_0 recomputed on chip (step kernel's feat0_recompute); bf16,
-// 256-wide layer 0, the 96-wide feat_0 of L = 13..16.  False if the shape does not qualify.
+// 256-wide layer 0, the 64-wide feat_0 of L <= 12 or the 96-wide one of L = 13..16 (both built in
+// the 96-wide stage, whose 192-B rows keep the transposed reads conflict-free; a 64-wide partial
+// takes its first 64 columns).  False if the shape does not qualify.
 bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk, int n_chunks, long long Np_pad) {
-    return M == 256 && ldz % 8 == 0 && ldz >= M && ldf0 == 96 && S % WG_SP0 == 0 && chunk % WG_SP0 == 0 &&
+    return M == 256 && ldz % 8 == 0 && ldz >= M && (ldf0 == 96 || ldf0 == 64) && S % WG_SP0 == 0 && chunk % WG_SP0 == 0 &&
            (long long)n_chunks <= 0x7fffffff && Np_pad < (1 << 24) && (chunk + Np_pad - 1) / Np_pad + 1 <= F0_PATCHES;
 }
 
 hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev& geo, const float* c2f_w, int L,
-                                          int nk0, long long S, int M, int chunk, int n_chunks, float* partial,
+                                          int nk0, int K0, long long S, int M, int chunk, int n_chunks, float* partial,
                                           float* bpartial, hipStream_t s, const WgRange* rng) {
     WgArgs a;
     memset(&a, 0, sizeof(a));
@@ -841,7 +844,7 @@ hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev&
     a.ldz = ldz;
     a.ldf = 96;
     a.M = M;
-    a.K = 96;
+    a.K = K0;  // partial columns: 96, or the first 64 of the 96-wide stage
     a.chunk = chunk;
     a.partial = partial;
     a.bpartial = bpartial;
@@ -866,7 +869,7 @@ bool marf_wgrad_fused_ok(const WgFusedLayer* layers, int n_layers, long long S, 
                     return false;
                 break;
             case 1:  // marf_launch_wgrad_l0_recompute's shape
-                if (!(L.K == 96 && marf_wgrad_l0_recompute_ok(L.M, L.ldz, 96, S, chunk, n_chunks, Np_pad))) return false;
+                if (!marf_wgrad_l0_recompute_ok(L.M, L.ldz, L.K, S, chunk, n_chunks, Np_pad)) return false;
                 ++n_l0;
                 break;
             case 2:  // layer 0 stored: any shape marf_launch_wgrad takes (its kernel is picked there)
@@ -893,7 +896,7 @@ hipError_t marf_launch_wgrad_fused(const WgFusedLayer* layers, int n_layers, lon
     if (l0) {
         if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(s2, fork, 0)) != hipSuccess) return e;
         if (l0->kind == 1)
-            e = marf_launch_wgrad_l0_recompute(l0->dz, l0->ldz, f0_geo, c2f_w, L, nk0, S, l0->M, chunk, n_chunks, l0->partial,
+            e = marf_launch_wgrad_l0_recompute(l0->dz, l0->ldz, f0_geo, c2f_w, L, nk0, l0->K, S, l0->M, chunk, n_chunks, l0->partial,
                                                l0->bpartial, s2);
         else
             e = marf_launch_wgrad(1, l0->dz, l0->ldz, l0->feat, l0->ldf, S, l0->M, l0->K, chunk, n_chunks, l0->partial,
