@@ -536,7 +536,10 @@ int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, vo
         mx = std::max(mx, (long long)p.Mp * p.Kp + (long long)p.Kp * p.Mt + p.Mp);
     }
     MarfProfScope ps("pack_weights", (hipStream_t)stream);
-    HIPCHK(marf_launch_pack(net->kdt, d_params, (char*)d_packed, a, mx, (hipStream_t)stream), "net_pack");
+    // the tile kernels' layouts (Wf / Wt / bias): every path of a split-bf16 net runs k_step2's
+    // program instead (marf_forward / marf_backward refuse it), so it packs that one only
+    if (net->dtype != MARF_BF16X3)
+        HIPCHK(marf_launch_pack(net->kdt, d_params, (char*)d_packed, a, mx, (hipStream_t)stream), "net_pack");
     if (net->s2.variant >= 0) {
         const Step2NetPlan& q = net->s2;
         Pack2Args b;
@@ -1260,10 +1263,27 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
             if (rc) return rc;
             {
                 std::lock_guard<std::mutex> hold(st->use);
+                if (d_dh) {
+                    // the warp gradient (one block: the dH partials' fixed-order sum + the Lie
+                    // backward) reads only the step kernel's partials and the upstream gradient: it
+                    // runs on the side stream ahead of layer 0, beside the hidden layers' gradients,
+                    // and the fused launch's join covers it
+                    HIPCHK(hipEventRecord(st->ev[2], s), "step_backward: fork");
+                    HIPCHK(hipStreamWaitEvent(st->s2, st->ev[2], 0), "step_backward: fork");
+                    MarfProfScope ps("warp_bwd_side", st->s2);
+                    HIPCHK(marf_launch_reduce_dH((const float*)(sv + p.dH), g.Np_pad / q.PX, g.B, d_h_params, nullptr,
+                                                 d_dh, lie_batch > 0 ? lie_batch : g.B, st->s2, d_gout, denom),
+                           "step_backward warp");
+                }
                 MarfProfScope ps("wgrad_fused", s);
                 HIPCHK(marf_launch_wgrad_fused(Lf, nf, p.S, (int)chunk, n_chunks, g, (const float*)(sv + p.c2f), net->L,
                                                q.nk0w, d_gout, denom, s, st->s2, st->ev[0], st->ev[1]),
                        "step_backward fused weight gradients");
+                if (d_dh) {  // (joined already when layer 0 ran on s2; an extra join is harmless)
+                    HIPCHK(hipEventRecord(st->ev[3], st->s2), "step_backward: join");
+                    HIPCHK(hipStreamWaitEvent(s, st->ev[3], 0), "step_backward: join");
+                    d_dh = nullptr;
+                }
             }
             for (int l = nl - 1; l >= 0; --l) {
                 rc = mark_layer(ev, l, s);

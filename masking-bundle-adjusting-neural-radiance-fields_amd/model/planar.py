@@ -29,6 +29,36 @@ from util import log
 from warp import Lie, Warp
 
 
+def _const_zero(t):
+    """The integer zeros compute_loss puts in for the absent mask / edge terms (torch.tensor(0) on
+    the CPU, as model/planar.py:374-378 does) -- never a computed loss (those are float tensors)."""
+    return (torch.is_tensor(t) and t.device.type == "cpu" and t.dim() == 0 and not t.is_floating_point()
+            and not t.requires_grad and int(t) == 0)
+
+
+def lin_comb(terms, start_zero=False):
+    """sum_i c_i * t_i in order ((start_zero: 0. + ...), the expression of model/planar.py:377 /
+    :180-183), without the operations that are exact identities in IEEE arithmetic: a factor of
+    exactly 1.0 (x * 1.0 == x), a term that is one of compute_loss's integer zero constants, and the
+    leading 0. + (x + 0 == x for every x but -0.0; these losses are >= +0 or NaN).  Same values, same
+    dtypes (fp32 * python float stays fp32; an int zero never promotes) and same gradients (d(x * 1)
+    = d(x + 0) = the upstream gradient), without one GPU launch per identity: 14 launches of scalar
+    arithmetic per training step become 3 (one add forward, the seed and one accumulation backward)."""
+    acc = None
+    for c, t in terms:
+        if _const_zero(t):
+            continue
+        x = t if (isinstance(c, (int, float)) and float(c) == 1.0) else c * t
+        acc = x if acc is None else acc + x
+    if acc is None:  # every term a constant zero: the plain expression
+        acc = 0. if start_zero else 0
+        for c, t in terms:
+            acc = acc + c * t
+    elif start_zero and not torch.is_tensor(acc):
+        acc = 0. + acc
+    return acc
+
+
 def _precision(opt):
     p = str(opt.get("precision", "fp32")).lower()
     if p in ("fp32", "float32", "f32"):
@@ -165,7 +195,6 @@ class Model(torch.nn.Module):
 
     def summarize_loss(self, loss):
         """all = sum_k 10^w_k loss_k with NaN / Inf checks (model/planar.py:172-185)."""
-        loss_all = 0.
         assert "all" not in loss
         for key in loss:
             assert key in self.opt.loss_weight
@@ -173,18 +202,15 @@ class Model(torch.nn.Module):
             if self.opt.loss_weight[key] is not None:
                 assert not torch.isinf(loss[key]), f"loss {key} is Inf"
                 assert not torch.isnan(loss[key]), f"loss {key} is NaN"
-                loss_all += 10 ** float(self.opt.loss_weight[key]) * loss[key]
-        loss.update(all=loss_all)
-        return loss
+        return self._loss_sum(loss)
 
     def _loss_sum(self, loss):
         """summarize_loss's weighted sum without its host-side NaN / Inf asserts (each one waits for
-        the GPU: a captured step must not synchronise; train_iteration checks at logging steps)."""
-        loss_all = 0.
-        for key in loss:
-            if self.opt.loss_weight[key] is not None:
-                loss_all += 10 ** float(self.opt.loss_weight[key]) * loss[key]
-        loss.update(all=loss_all)
+        the GPU: a captured step must not synchronise; train_iteration checks at logging steps).
+        0. + sum_k 10^w_k loss_k in key order, through lin_comb: the same values and gradients."""
+        terms = [(10 ** float(self.opt.loss_weight[key]), loss[key]) for key in loss
+                 if self.opt.loss_weight[key] is not None]
+        loss.update(all=lin_comb(terms, start_zero=True))
         return loss
 
     def graph_capable(self):
@@ -501,7 +527,7 @@ class Graph(torch.nn.Module):
             else:
                 edge_loss = torch.tensor(0)
             mask_loss = torch.tensor(0)
-            loss.render = (1 - alpha) * rgb_loss + 0.5 * mask_loss + alpha * edge_loss
+            loss.render = lin_comb([(1 - alpha, rgb_loss), (0.5, mask_loss), (alpha, edge_loss)])
             loss.rgb = rgb_loss
             loss.mask = mask_loss
             loss.edge = edge_loss

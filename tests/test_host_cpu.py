@@ -1,0 +1,50 @@
+"""Host-side logic of the training step that needs no GPU: the loss composition of
+Graph.compute_loss / Model.summarize_loss (model/planar.py:374-378, 172-185 of the reference)."""
+import itertools
+
+import pytest
+import torch
+
+
+def _plain(terms, start_zero=False):
+    acc = 0. if start_zero else None
+    for c, t in terms:
+        acc = c * t if acc is None else acc + c * t
+    return acc
+
+
+@pytest.mark.parametrize("alpha,edge,w", list(itertools.product(
+    [0, 0.0, 0.37], ["const", "fp64", "fp64-zero"], [0.0, -1.0, 0.5])))
+def test_lin_comb_is_the_plain_expression(alpha, edge, w):
+    """lin_comb drops x * 1.0, the integer zero constants and the leading 0. + (exact identities):
+    the render and total losses and the gradient reaching rgb_loss are bitwise the reference
+    expression's, in the same dtype."""
+    from model.planar import lin_comb
+    g = torch.Generator().manual_seed(7)
+    for trial in range(5):
+        v = torch.rand((), generator=g, dtype=torch.float32) * 10 ** trial
+        outs = []
+        for f in (_plain, lin_comb):
+            rgb = v.clone().requires_grad_()
+            e = (torch.tensor(0) if edge == "const" else
+                 torch.zeros((), dtype=torch.float64) if edge == "fp64-zero" else
+                 (torch.rand((), generator=torch.Generator().manual_seed(trial), dtype=torch.float64)))
+            m = torch.tensor(0)
+            render = f([(1 - alpha, rgb), (0.5, m), (alpha, e)])
+            weights = {"render": 10 ** w, "rgb": 10 ** 0.0, "mask": 1.0, "edge": 10 ** w}
+            loss = {"render": render, "rgb": rgb, "mask": m, "edge": e}
+            total = f([(weights[k], loss[k]) for k in loss], start_zero=True)
+            total.backward()
+            outs.append((render.detach(), total.detach(), rgb.grad.clone()))
+        for a, b in zip(*outs):
+            assert a.dtype == b.dtype
+            assert torch.equal(a.view(-1).view(torch.int64 if a.dtype == torch.float64 else torch.int32),
+                               b.view(-1).view(torch.int64 if b.dtype == torch.float64 else torch.int32))
+
+
+def test_lin_comb_all_zero_terms_keep_the_plain_result():
+    from model.planar import lin_comb
+    z = torch.tensor(0)
+    assert lin_comb([(1.0, z), (0.5, z)]) == 0
+    r = lin_comb([(1.0, z)], start_zero=True)
+    assert float(r) == 0.0
