@@ -1263,31 +1263,37 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
             if (rc) return rc;
             {
                 std::lock_guard<std::mutex> hold(st->use);
-                if (d_dh) {
-                    // the warp gradient (one block: the dH partials' fixed-order sum + the Lie
-                    // backward) reads only the step kernel's partials and the upstream gradient: it
-                    // runs on the side stream ahead of layer 0, beside the hidden layers' gradients,
-                    // and the fused launch's join covers it
+                const char* dse = getenv("MARF_DH_SIDE");  // A/B switch (per launch): 0 = after the reductions on s
+                float* dh_side = (dse && dse[0] == '0') ? nullptr : d_dh;
+                if (dh_side) {  // s2 joins the step here (the fused launch forks it again for layer 0)
                     HIPCHK(hipEventRecord(st->ev[2], s), "step_backward: fork");
                     HIPCHK(hipStreamWaitEvent(st->s2, st->ev[2], 0), "step_backward: fork");
+                }
+                {
+                    MarfProfScope ps("wgrad_fused", s);
+                    HIPCHK(marf_launch_wgrad_fused(Lf, nf, p.S, (int)chunk, n_chunks, g, (const float*)(sv + p.c2f),
+                                                   net->L, q.nk0w, d_gout, denom, s, st->s2, st->ev[0], st->ev[1]),
+                           "step_backward fused weight gradients");
+                }
+                if (dh_side) {
+                    // the warp gradient (one block: the dH partials' fixed-order sum + the Lie
+                    // backward) reads only the step kernel's partials and the upstream gradient: it
+                    // follows layer 0 on the side stream (ahead of it, it would hold layer 0 back
+                    // until the hidden layers free a CU) and runs beside the reductions
                     MarfProfScope ps("warp_bwd_side", st->s2);
                     HIPCHK(marf_launch_reduce_dH((const float*)(sv + p.dH), g.Np_pad / q.PX, g.B, d_h_params, nullptr,
-                                                 d_dh, lie_batch > 0 ? lie_batch : g.B, st->s2, d_gout, denom),
+                                                 dh_side, lie_batch > 0 ? lie_batch : g.B, st->s2, d_gout, denom),
                            "step_backward warp");
-                }
-                MarfProfScope ps("wgrad_fused", s);
-                HIPCHK(marf_launch_wgrad_fused(Lf, nf, p.S, (int)chunk, n_chunks, g, (const float*)(sv + p.c2f), net->L,
-                                               q.nk0w, d_gout, denom, s, st->s2, st->ev[0], st->ev[1]),
-                       "step_backward fused weight gradients");
-                if (d_dh) {  // (joined already when layer 0 ran on s2; an extra join is harmless)
                     HIPCHK(hipEventRecord(st->ev[3], st->s2), "step_backward: join");
+                }
+                for (int l = nl - 1; l >= 0; --l) {  // (ahead of the warp gradient's join: the
+                    rc = mark_layer(ev, l, s);        //  layers' all-reduces do not wait for it)
+                    if (rc) return rc;
+                }
+                if (dh_side) {
                     HIPCHK(hipStreamWaitEvent(s, st->ev[3], 0), "step_backward: join");
                     d_dh = nullptr;
                 }
-            }
-            for (int l = nl - 1; l >= 0; --l) {
-                rc = mark_layer(ev, l, s);
-                if (rc) return rc;
             }
             d_dparams = nullptr;  // done
         }

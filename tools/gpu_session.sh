@@ -9,6 +9,7 @@
 #   bits                      tools/make_step2_bits.py -> <tag>/step2_bits.json
 #   ab=<v1,v2,...>            C3 bench of lib/libmarf_<v>.so variants ("default" = lib/libmarf.so),
 #                             alternating twice (timing-only variants: MARF_AB_TIMING_ONLY=1)
+#   envab=VAR:v1,v2[:c1,c3]   C1 / C3 benches with VAR=v1, v2, ... alternating twice (library A/B switches)
 #   cfg                       secondary bench lines (tools/bench_configs.sh)
 #   pmc=<config>/<precision>  FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh)
 # Every GPU step has its own time limit; the session stops at the first failure, abort or timeout.
@@ -59,6 +60,22 @@ for step in "$@"; do
           MARF_LIB=$L MARF_AB_TIMING_ONLY=$TO timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render \
             > $OUT/ab_$v.json 2> $OUT/ab_$v.err || { echo "ab $v failed"; tail -5 $OUT/ab_$v.err; exit 1; }
           line $OUT/ab_$v.json "$v"
+        done
+      done ;;
+    envab=*)
+      # envab=VAR:v1,v2[:c1,c3]  C1 / C3 benches of the product library with VAR=v1, VAR=v2, ...
+      # alternating twice (A/B switches of the library read per launch)
+      SPEC=${step#envab=}; VAR=${SPEC%%:*}; REST=${SPEC#*:}; VALS=${REST%%:*}; CFGS=c1,c3
+      [ "$REST" != "$VALS" ] && CFGS=${REST#*:}
+      IFS=, read -ra VS <<< "$VALS"; IFS=, read -ra CS <<< "$CFGS"
+      for rep in 1 2; do
+        for v in "${VS[@]}"; do
+          for c in "${CS[@]}"; do
+            if [ $c = c1 ]; then A=(--config c1 --precision bf16x3 --steps 30 --warmup 3); else A=(--config $c --steps 10 --warmup 2); fi
+            env $VAR=$v timeout -k 10 200 python bench.py "${A[@]}" --no-cpu-baseline --no-render \
+              > $OUT/envab_${c}_$v.json 2> $OUT/envab_${c}_$v.err || { echo "envab $c $v failed"; tail -5 $OUT/envab_${c}_$v.err; exit 1; }
+            line $OUT/envab_${c}_$v.json "$c $VAR=$v"
+          done
         done
       done ;;
     cfg)
