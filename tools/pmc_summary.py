@@ -76,6 +76,8 @@ if "--traffic" in sys.argv:
             name = "mlp_step"
         elif k.startswith("k_prologue_probe"):
             name = "prologue_probe"
+        elif k.startswith("k_wgrad_dma_layers<"):  # every hidden layer in one launch (fused path)
+            name = "wgrad_hidden"
         elif k.startswith("k_wgrad_dma<"):
             name = "wgrad_l0" if ", 96" in k else "wgrad_hidden"
         elif k.startswith("k_wgrad<"):
