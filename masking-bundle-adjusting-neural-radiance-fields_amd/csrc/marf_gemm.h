@@ -504,7 +504,7 @@ template <class P, int RT, int PT, int NW = 4>
 MARF_DEV void dgrad_epilogue(f32x16 (&acc)[RT][PT], const NetDev& net, int l, typename P::T* act, int lda, int wave,
                              int lane, uint4 mw, float* dsk) {
     const int R = net.Kp[l];
-    if ((net.skip >> l) & 1u) {
+    if (dsk && ((net.skip >> l) & 1u)) {  // (dsk: null in kernels built without skip support)
         mask_epilogue<P, RT, PT, NW>(acc, act, lda, net.Mp[l - 1] / 32, wave, lane, mw, net.diag[l - 1]);
         skip_epilogue<P, RT, PT, NW>(acc, dsk, net.Kp[0], net.Mp[l - 1] / 32, R / 32, wave, lane);
     } else {

@@ -24,7 +24,9 @@ namespace marf {
 
 // ======================================================================== forward
 
-template <class P, int TP>
+// SK: the net has skip layers (their posenc prologue is compiled in only then: it costs the plain
+// nets registers and spills)
+template <class P, int TP, bool SK>
 __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
     typedef typename P::T T;
     constexpr int PT = TP / 32;
@@ -58,7 +60,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(FwdArgs a) {
         __syncthreads();  // every wave has consumed the layer input
         relu_epilogue<P, RT, PT>(acc, act, lda, n_rt, wave, lane, a.mask[l + 1], blockIdx.x, net.diag[l + 1]);
         __syncthreads();
-        if ((net.skip >> (l + 1)) & 1u) {  // skip layer: [feature ; posenc] (model/planar.py:440-441)
+        if (SK && ((net.skip >> (l + 1)) & 1u)) {  // skip layer: [feature ; posenc] (model/planar.py:440-441)
             tile_prologue<P, TP>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0, M);
             __syncthreads();
         }
@@ -181,14 +183,19 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(BwdArgs a) {
 
 using namespace marf;
 
-template <class P, int TP>
-static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, int n_tiles, hipStream_t s) {
+template <class P, int TP, bool SK>
+static hipError_t launch_fwd_sk(const FwdArgs& a, size_t lds, int n_tiles, hipStream_t s) {
     {
-        hipError_t e = ensure_dynamic_lds((const void*)k_mlp_fwd<P, TP>, lds);
+        hipError_t e = ensure_dynamic_lds((const void*)k_mlp_fwd<P, TP, SK>, lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((k_mlp_fwd<P, TP>), dim3(n_tiles), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_mlp_fwd<P, TP, SK>), dim3(n_tiles), dim3(256), lds, s, a);
     return hipGetLastError();
+}
+
+template <class P, int TP>
+static hipError_t launch_fwd_t(const FwdArgs& a, size_t lds, int n_tiles, hipStream_t s) {
+    return a.net.skip ? launch_fwd_sk<P, TP, true>(a, lds, n_tiles, s) : launch_fwd_sk<P, TP, false>(a, lds, n_tiles, s);
 }
 
 template <class P, int TP>

@@ -40,7 +40,9 @@ constexpr int MARF_STEP_NBIAS = 1024;
 // NW = waves per block: 4 (two blocks per CU) or 8 (one 512-thread block per CU, two waves per
 // SIMD: the 512-wide C5 net at TP = 128, where every weight fragment a wave loads from L2 feeds 4
 // pixel tiles' MFMAs instead of 2 -- half the weight-fragment traffic per MFMA of TP = 64)
-template <class P, int TP, bool BL, int NW>
+// SK: the net has skip layers (their prologue / posenc-gradient code is compiled in only then: it
+// costs the plain nets registers and spills)
+template <class P, int TP, bool BL, int NW, bool SK>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs a) {
     typedef typename P::T T;
     constexpr int PT = TP / 32;
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
         relu_epilogue<P, RT, PT, NW>(acc, act, lda, n_rt, wave, lane, a.mask_bits[l + 1], blockIdx.x, net.diag[l + 1]);
         __syncthreads();
         if (l < 3) STAMP(3 + 2 * l);
-        if ((net.skip >> (l + 1)) & 1u) {  // skip layer: [feature ; posenc] (model/planar.py:440-441)
+        if (SK && ((net.skip >> (l + 1)) & 1u)) {  // skip layer: [feature ; posenc] (model/planar.py:440-441)
             tile_prologue<P, TP, true, NW>(net, a.geo, a.c2f.on, wsh, act, lda, b, p0, M);
             __syncthreads();
         }
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
     // ---- dgrad chain, l = n-1 .. 1 : dfeat_l = W_l^T dz_{l+1}; dz_l = dfeat_l * relu'(feat_l)
     st.clear();
     float* dsk = nullptr;  // skip nets: the posenc gradient of the skip layers
-    if (net.skip) {
+    if (SK && net.skip) {
         dsk = reinterpret_cast<float*>(smem + skip_lds_off<P, TP>(net, lda));
         for (int e = threadIdx.x; e < TP * net.Kp[0]; e += 64 * NW) dsk[e] = 0.f;
     }
@@ -370,14 +372,20 @@ __global__ __launch_bounds__(256) void k_loss_final(const double* __restrict__ p
 
 using namespace marf;
 
-template <class P, int TP, bool BL, int NW>
-static hipError_t launch_step_t(const StepArgs& a, size_t lds, int n_tiles, hipStream_t s) {
+template <class P, int TP, bool BL, int NW, bool SK>
+static hipError_t launch_step_sk(const StepArgs& a, size_t lds, int n_tiles, hipStream_t s) {
     {
-        hipError_t e = ensure_dynamic_lds((const void*)k_mlp_step<P, TP, BL, NW>, lds);
+        hipError_t e = ensure_dynamic_lds((const void*)k_mlp_step<P, TP, BL, NW, SK>, lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((k_mlp_step<P, TP, BL, NW>), dim3(n_tiles), dim3(64 * NW), lds, s, a);
+    hipLaunchKernelGGL((k_mlp_step<P, TP, BL, NW, SK>), dim3(n_tiles), dim3(64 * NW), lds, s, a);
     return hipGetLastError();
+}
+
+template <class P, int TP, bool BL, int NW>
+static hipError_t launch_step_t(const StepArgs& a, size_t lds, int n_tiles, hipStream_t s) {
+    return a.net.skip ? launch_step_sk<P, TP, BL, NW, true>(a, lds, n_tiles, s)
+                      : launch_step_sk<P, TP, BL, NW, false>(a, lds, n_tiles, s);
 }
 
 template <class P, int TP, int NW>
