@@ -1149,9 +1149,10 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     off += q.NW * a.lds_wave_bytes;
     a.lds_total = off;
     if (off > 160 * 1024) return fail(MARF_ERR_UNSUPPORTED, "step2: LDS plan %d B exceeds 160 KB", off);
-    if (net->L > 0) HIPCHK(marf_launch_c2f_weights(cf, net->L, (float*)(sv + p.c2f), s), "step_forward c2f");
-    HIPCHK(hipMemcpyAsync(sv + p.kmap, pk + q.kmap_off, (size_t)net->D * 4, hipMemcpyDeviceToDevice, s),
-           "step_forward kmap");
+    // the band weights and the layer-0 column map (packed buffer -> saved buffer) in one launch
+    HIPCHK(marf_launch_c2f_weights(cf, net->L, (float*)(sv + p.c2f), s, (const int*)(pk + q.kmap_off),
+                                   (int*)(sv + p.kmap), net->D),
+           "step_forward c2f / kmap");
     if (render) {
         MarfProfScope ps("mlp_fwd", s);
         HIPCHK(launch_s2(net, a, p.grid, s), "render step2");

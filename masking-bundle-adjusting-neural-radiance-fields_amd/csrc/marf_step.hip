@@ -332,8 +332,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mlp_step(StepArgs 
 }
 
 // The step's c2f band weights, once (model/planar.py:462-470; 1 without c2f).
-__global__ void k_c2f_weights(C2fDev c, int L, float* __restrict__ out) {
+// (+ an optional int copy riding along: the step kernel's layer-0 column map, one launch fewer)
+__global__ void k_c2f_weights(C2fDev c, int L, float* __restrict__ out, const int* __restrict__ csrc,
+                              int* __restrict__ cdst, int cn) {
     if ((int)threadIdx.x < L) out[threadIdx.x] = c.on ? c2f_weight(*c.progress, c.start, c.span, L, threadIdx.x) : 1.0f;
+    for (int i = threadIdx.x; i < cn; i += blockDim.x) cdst[i] = csrc[i];
 }
 
 // Loss of the fused step from the per-tile partials (fp64, fixed-order tree):
@@ -411,8 +414,9 @@ hipError_t marf_launch_mlp_step(const StepArgs& a, int dtype, int TP, int NW, si
     return TP == 128 ? launch_step_b<PrecF32, 128, 4>(a, lds, n_tiles, s) : launch_step_b<PrecF32, 64, 4>(a, lds, n_tiles, s);
 }
 
-hipError_t marf_launch_c2f_weights(const C2fDev& c, int L, float* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_c2f_weights, dim3(1), dim3(64), 0, s, c, L, out);
+hipError_t marf_launch_c2f_weights(const C2fDev& c, int L, float* out, hipStream_t s, const int* csrc, int* cdst,
+                                   int cn) {
+    hipLaunchKernelGGL(k_c2f_weights, dim3(1), dim3(64), 0, s, c, L, out, csrc, cdst, cn);
     return hipGetLastError();
 }
 
