@@ -1144,8 +1144,14 @@ def _bits_fixture():
     return json.load(open(step_bits.BITS_JSON))
 
 
+# the library's A/B switches (read per launch): each must give the default path's bits
+_BITS_SWITCHES = {"generic": ("MARF_STEP2_GENERIC", "1"), "perlayer": ("MARF_WGRAD_FUSED", "0"),
+                  "dhlast": ("MARF_DH_SIDE", "0"), "f0stored": ("MARF_F0_RECOMPUTE", "0")}
+
+
 @pytest.mark.parametrize("case", ["c1", "c3x2", "c3x3-L10", "L16-1tile", "narrow", "L13", "L15", "c1-generic",
-                                  "c3x2-generic"])
+                                  "c3x2-generic", "c1-perlayer", "c3x2-perlayer", "c1-dhlast", "c1-f0stored",
+                                  "c3x2-f0stored"])
 def test_step2_bits_unchanged(case, monkeypatch):
     """The split-bf16 step computes the bits the seed-3 run was pinned on: rgb, loss, every MLP
     gradient and d warp of one fused step, then the losses, warps and weights after two more
@@ -1153,12 +1159,15 @@ def test_step2_bits_unchanged(case, monkeypatch):
     MI355X by tools/make_step2_bits.py from the round-4 library, commit d3c2143).  Covers every
     compile-time instantiation of k_step2 (L = 8, 9..12, 13..15, 16), the generic kernel (narrow
     widths) and one tile per block; "-generic": the same case on the generic kernel
-    (MARF_STEP2_GENERIC=1), which must give the instantiation's bits.  (The 64-patch headline
-    case: test_c3_headline_step.)"""
+    (MARF_STEP2_GENERIC=1), which must give the instantiation's bits; "-perlayer" / "-dhlast" /
+    "-f0stored": the per-layer weight-gradient launches, the warp gradient after the reductions,
+    feat_0 stored and read instead of recomputed.  (The 64-patch headline case:
+    test_c3_headline_step.)"""
     import step_bits
-    if case.endswith("-generic"):
-        case = case[:-len("-generic")]
-        monkeypatch.setenv("MARF_STEP2_GENERIC", "1")
+    for suffix, (var, val) in _BITS_SWITCHES.items():
+        if case.endswith("-" + suffix):
+            case = case[:-len(suffix) - 1]
+            monkeypatch.setenv(var, val)
     ref = _bits_fixture()["cases"][case]
     got = step_bits.case_bits(case)
     bad = sorted(k for k in ref["bits"] if got["bits"].get(k) != ref["bits"][k])
