@@ -1061,7 +1061,7 @@ static int wgrad_piece(const marf_net* net, const GeoDev& g, const Step2BufPlan&
                    "step_forward pipelined wgrad_l0");
         else
             HIPCHK(marf_launch_wgrad(1, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K, 32, r.n,
-                                     part, bpart, s2, &r),
+                                     part, bpart, s2, &r, true),
                    "step_forward pipelined wgrad");
     }
     return MARF_OK;
@@ -1339,7 +1339,7 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                            "step_backward wgrad_l0 (feat_0 recomputed)");
                 else
                     HIPCHK(marf_launch_wgrad(1, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K,
-                                             (int)chunk, n_chunks, part, bpart, s),
+                                             (int)chunk, n_chunks, part, bpart, s, nullptr, true),
                            "step_backward wgrad");
             }
             {

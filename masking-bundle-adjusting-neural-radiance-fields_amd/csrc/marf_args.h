@@ -152,9 +152,10 @@ bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk
 hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev& geo, const float* c2f_w, int L,
                                           int nk0, int K0, long long S, int M, int chunk, int n_chunks, float* partial,
                                           float* bpartial, hipStream_t s, const WgRange* rng = nullptr);
+// t16: dz / feat in the split-recipe step kernel's T16 block layout (marf_wgrad.hip t16_off)
 hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
                              int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s,
-                             const WgRange* rng = nullptr);
+                             const WgRange* rng = nullptr, bool t16 = false);
 // One layer of the fused weight-gradient launch (marf_launch_wgrad_fused): its split-K partials
 // [n_parts][M][K] (+ [n_parts][M] bias) and the fixed-order reduction into dW [Mo][Ko] / db [Mo].
 struct WgFusedLayer {

@@ -341,12 +341,15 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
 
     S2Frag Bh[NKH], Bl[NKH], Oh[NKH], Ol[NKH];
 
-    // (the stores of a row tile into a natural-order [S][ld] bf16 tensor: k-step ks of the lane's
-    //  pixel holds columns 16 ks + 4 h + 0..3 (dwords x, y) and 16 ks + 8 + 4 h + 0..3 (z, w); two
+    // (the stores of a row tile into a saved tensor in the T16 block layout (marf_wgrad.hip
+    //  t16_off: 32 pixels x 16 features per 1 KB block): k-step ks of the lane's pixel holds
+    //  columns 16 ks + 4 h + 0..3 (dwords x, y) and 16 ks + 8 + 4 h + 0..3 (z, w); two
     //  v_permlane32_swap exchange the lane halves' x, y <-> z, w so that lane (p, h) holds columns
-    //  16 ks + 8 h + 0..7 contiguously: one 16-B store per lane per k-step, 2 per row tile)
-    //  row0 = the lane's row base (tensor + slot * ld + 8 h), the row tile's column offset is the
-    //  stores' instruction offset)
+    //  16 ks + 8 h + 0..7 contiguously: one 16-B store per lane per k-step, and the 64 lanes' stores
+    //  of k-step ks fill feature block ks of the set's 32 pixels, 1 KB contiguous (a row-major
+    //  [S][ld] tensor took 32 segments of 32 B per instruction).  row0 = the lane's base in the
+    //  set's block row (tensor + (slot0 / 32) * ld * 32 + pixel * 16 + 8 h); row tile rt = blocks
+    //  2 rt, 2 rt + 1)
     auto store_rt = [&](u16* row0, auto rtc, const S2Frag& f0, const S2Frag& f1) {
         constexpr int rt = decltype(rtc)::value;
         auto contig = [&](const S2Frag& f) -> uint4 {
@@ -354,8 +357,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const auto yw = __builtin_amdgcn_permlane32_swap(f.u.y, f.u.w, false, false);
             return make_uint4(xz[0], yw[0], xz[1], yw[1]);
         };
-        s2_st16o<64 * rt>(row0, contig(f0));
-        s2_st16o<64 * rt + 32>(row0, contig(f1));
+        u16* blk = row0 + 1024 * rt;  // (2 KB per row tile: past the 12-bit instruction offset)
+        s2_st16o<0>(blk, contig(f0));
+        s2_st16o<1024>(blk, contig(f1));
         st_cur += 2;
     };
 
@@ -679,7 +683,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const int b = tile / tpp;
             const int p0 = (tile - b * tpp) * C::TPX + 32 * wave;
             const long long slot0 = (long long)b * a.geo.Np_pad + p0;
-            const long long myslot = slot0 + pxl;
             const int p = p0 + pxl;
             const bool valid = p < Np;
             const float* pro = pro_buf(pb);
@@ -741,14 +744,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 // feat_0 (bf16 hi) for the layer-0 weight gradient: column 16 ks + 8 h + j
                 // (every armed DMA piece was issued before the previous store: these count as the
                 //  current stage's stores)
-                if (!a.fwd_only && !a.feat0_recompute) {
-                    u16* row = ly_ptr(0, 0) + myslot * ly_int(0, 3);
+                if (!a.fwd_only && !a.feat0_recompute) {  // (T16: k-step g = feature block g)
+                    u16* row = ly_ptr(0, 0) + (slot0 >> 5) * ly_int(0, 3) * 32 + pxl * 16 + 8 * h;
 #pragma unroll
                     for (int g = 0; g < C::NK0; ++g)
-                        if (g < nk0) s2_st16(row + 16 * g + 8 * h, F0h[g].u);
+                        if (g < nk0) s2_st16(row + 512 * g, F0h[g].u);
                     st_cur += nk0;
                     if (16 * nk0 < ly_int(0, 3)) {
-                        s2_st16(row + 16 * nk0 + 8 * h, make_uint4(0, 0, 0, 0));
+                        s2_st16(row + 512 * nk0, make_uint4(0, 0, 0, 0));
                         st_cur += 1;
                     }
                 }
@@ -765,7 +768,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 constexpr bool SPLITPK = SPLIT && MS == 1 && decltype(nk_tag)::value == NKH;  // hidden, split recipe
                 const int nrt = FIX ? NRT : ly_int(l, 0);
                 const bool save = l + 1 < nl - 1 && !a.fwd_only;
-                u16* srow = save ? ly_ptr(l + 1, 0) + myslot * ly_int(l + 1, 3) + 8 * h : nullptr;
+                u16* srow = save ? ly_ptr(l + 1, 0) + (slot0 >> 5) * ly_int(l + 1, 3) * 32 + pxl * 16 + 8 * h : nullptr;
                 const int boff = ly_int(l, 2);
                 const char* slot0 = nullptr;
                 s2_sfor<NRT>([&](auto rtc) {
@@ -980,7 +983,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             }
             sl0[s] = v;
         });
-        auto myslot_of = [&](int s) -> long long { return sl0[s] + pxl; };
         // operand / output fragments of set s: the forward's arrays (the dgrad needs hi only, so the
         // lo arrays carry the second set; reusing them keeps no extra array live across the pass)
         S2Frag* const Dh[2] = {Bh, Bl};
@@ -994,7 +996,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const int nrt = FIX ? NRT : ly_int(nl - 1, 1);
             u16* brow[NS];
             s2_sfor<NS>([&](auto sc) {
-                brow[decltype(sc)::value] = ly_ptr(nl - 1, 1) + myslot_of(decltype(sc)::value) * ly_int(nl - 1, 4) + 8 * h;
+                brow[decltype(sc)::value] = ly_ptr(nl - 1, 1) + (sl0[decltype(sc)::value] >> 5) * ly_int(nl - 1, 4) * 32 + pxl * 16 + 8 * h;
             });
             S2Frag gB[NS];
             s2_sfor<NS>([&](auto sc) { gB[decltype(sc)::value] = ss[decltype(sc)::value].g; });
@@ -1051,7 +1053,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const int nrt = FIX ? NRT : ly_int(l, 1);
             u16* brow[NS];
             s2_sfor<NS>([&](auto sc) {
-                brow[decltype(sc)::value] = ly_ptr(l, 1) + myslot_of(decltype(sc)::value) * ly_int(l, 4) + 8 * h;
+                brow[decltype(sc)::value] = ly_ptr(l, 1) + (sl0[decltype(sc)::value] >> 5) * ly_int(l, 4) * 32 + pxl * 16 + 8 * h;
             });
             s2_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;

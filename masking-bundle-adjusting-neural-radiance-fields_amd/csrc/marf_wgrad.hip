@@ -48,6 +48,7 @@ struct WgArgs {
     // part0 + c -- one piece of a pipelined step (marf_abi.hip, step2_forward)
     long long s_lo, s_len;
     int rng_n, part0;
+    int t16;           // dz / feat in the step kernel's T16 block layout (t16_off), not row-major
 };
 
 template <int RT, int CT>
@@ -58,6 +59,23 @@ struct WgGeo {
 
 MARF_DEV i16x4 tr_read(const u16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(p));
+}
+
+// T16: the layout the split-recipe step kernel saves feat_l / dz_l in (marf_step2.hip store_rt):
+// blocks of 32 pixels x 16 features (1 KB, pixel-major inside), the feature blocks of a 32-pixel
+// row of tiles consecutive, so each of the step kernel's 16-B lane stores lands in one contiguous
+// 1 KB per wave instruction (the row-major layout gave 32 segments of 32 B).  Element (p, f) of an
+// [S][ld] tensor (S multiple of 32, ld of 16):
+MARF_DEV size_t t16_off(long long p, int f, int ld) {
+    return ((size_t)(p >> 5) * (size_t)(ld >> 4) + (size_t)(f >> 4)) * 512 + (size_t)(p & 31) * 16 + (f & 15);
+}
+// ... and in a stage of the LDS-DMA ring: the same 1 KB blocks, nb per 32-row group, as they
+// stand (each DMA instruction copies one block, lanes in address order).  A row permutation that
+// took the transposed reads' bank conflicts out (through the lanes' source addresses) cost more in
+// the DMA than the conflicts did: hidden layers 2.61 -> 2.84 ms at C3 (profiles/r7e, same box)
+MARF_DEV int t16_lds(int r, int c, int nb) {  // byte offset of (stage row r, feature c)
+    const int b = c >> 4;
+    return ((r >> 5) * nb + b) * 1024 + (r & 31) * 32 + (c & 15) * 2;
 }
 
 // the product of pixel chunk `chunk_id` into output block `ob` (the body of one k_wgrad block;
@@ -97,14 +115,16 @@ MARF_DEV void wgrad_body(const WgArgs& a, int chunk_id, int ob, char* smem) {
             const int e = threadIdx.x + 512 * q;
             const int r = e / (BM / VEC), c = (e % (BM / VEC)) * VEC;
             rz[q] = make_uint4(0, 0, 0, 0);
-            if (s0 + r < s_end && m0 + c < a.M) rz[q] = *reinterpret_cast<const uint4*>(dz + (s0 + r) * a.ldz + m0 + c);
+            if (s0 + r < s_end && m0 + c < a.M)
+                rz[q] = *reinterpret_cast<const uint4*>(dz + (a.t16 ? t16_off(s0 + r, m0 + c, a.ldz) : (size_t)((s0 + r) * a.ldz + m0 + c)));
         }
 #pragma unroll
         for (int q = 0; q < NVF; ++q) {
             const int e = threadIdx.x + 512 * q;
             const int r = e / (BN / VEC), c = (e % (BN / VEC)) * VEC;
             rf[q] = make_uint4(0, 0, 0, 0);
-            if (s0 + r < s_end && k0 + c < a.K) rf[q] = *reinterpret_cast<const uint4*>(ft + (s0 + r) * a.ldf + k0 + c);
+            if (s0 + r < s_end && k0 + c < a.K)
+                rf[q] = *reinterpret_cast<const uint4*>(ft + (a.t16 ? t16_off(s0 + r, k0 + c, a.ldf) : (size_t)((s0 + r) * a.ldf + k0 + c)));
         }
     };
     auto store_stage = [&]() {
@@ -245,6 +265,7 @@ MARF_DEV int swz(int r, int c) {  // byte offset of bf16 element (r, c) in a 256
     return r * 512 + ((((c >> 3) ^ (4 * (r & 3)))) << 4) + (c & 7) * 2;
 }
 
+
 template <int N>
 MARF_DEV void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -261,7 +282,7 @@ MARF_DEV int foff(int r, int c) {
 
 // chunk `chunk_id` into output block `ob` (the body of one k_wgrad_dma block; also a work item of
 // k_wgrad_fused)
-template <class P, int NBUF, int SP, int KF, bool F0 = false>
+template <class P, int NBUF, int SP, int KF, bool F0 = false, bool T16 = false>
 MARF_DEV void wgrad_dma_body(const WgArgs& a, int chunk_id, int ob, char* smem) {
     static_assert(KF == 256 || KF == 96, "feat width");
     static_assert(!F0 || (KF == 96 && SP % 32 == 0), "feat_0 recompute: the 96-wide layer-0 stage, 32-row blocks");
@@ -382,12 +403,33 @@ MARF_DEV void wgrad_dma_body(const WgArgs& a, int chunk_id, int ob, char* smem) 
         }
       }
     };
+    // T16 sources: 1 KB instruction seg = block seg % nb of 32-row group seg / nb, lane L its bytes
+    // 16 L .. 16 L + 15 (stage-invariant: computed once per instruction slot q; a stage adds the
+    // base of its 32-row group)
+    auto t16_lane = [&](int ld, int blk0, int nb, int seg) -> unsigned {
+        const int tr = seg / nb, b = seg - tr * nb;
+        return ((unsigned)tr * (unsigned)(ld >> 4) + (unsigned)(blk0 + b)) * 1024u + (unsigned)lane * 16u;
+    };
+    unsigned t16z[NGZ > 0 ? NGZ : 1], t16f[NGF > 0 ? NGF : 1];
+    if constexpr (T16) {
+#pragma unroll
+        for (int q = 0; q < NGZ; ++q) t16z[q] = t16_lane(a.ldz, m0 >> 4, 16, q * 8 + wave);
+#pragma unroll
+        for (int q = 0; q < NGF; ++q) t16f[q] = t16_lane(a.ldf, k0 >> 4, KF >> 4, q * 8 + wave < (FB >> 10) ? q * 8 + wave : 0);
+    }
     auto issue = [&](int st) {
         const unsigned buf = lds0 + (st % NBUF) * STB;
         const long long row0 = s_begin + (long long)st * SP;
+        // T16: the stage's first 32-row group (wave-uniform)
+        const char* z16 = reinterpret_cast<const char*>(a.dz) + (size_t)(row0 >> 5) * (size_t)(a.ldz >> 4) * 1024;
+        const char* f16 = reinterpret_cast<const char*>(a.feat) + (size_t)(row0 >> 5) * (size_t)(a.ldf >> 4) * 1024;
 #pragma unroll
         for (int q = 0; q < NGZ; ++q) {
             const int seg = q * 8 + wave;         // 1 KB = 2 rows per wave instruction
+            if constexpr (T16) {
+                glds16(z16 + t16z[q], __builtin_amdgcn_readfirstlane(buf + seg * 1024));
+                continue;
+            }
             const int r = seg * 2 + (lane >> 5);
             const int c16 = (lane & 31) ^ (4 * (r & 3));
             glds16(dz + (size_t)(row0 + r) * ldzb + c16 * 16, __builtin_amdgcn_readfirstlane(buf + seg * 1024));
@@ -395,7 +437,10 @@ MARF_DEV void wgrad_dma_body(const WgArgs& a, int chunk_id, int ob, char* smem) 
 #pragma unroll
         for (int q = 0; q < NGF; ++q) {
             const int seg = q * 8 + wave;
-            if constexpr (KF == 256) {
+            if constexpr (T16) {
+                const bool real = seg * 1024 < FB;
+                glds16(f16 + t16f[q], __builtin_amdgcn_readfirstlane(real ? buf + ZB + seg * 1024 : junk));
+            } else if constexpr (KF == 256) {
                 const int r = seg * 2 + (lane >> 5);
                 const int c16 = (lane & 31) ^ (4 * (r & 3));
                 glds16(ft + (size_t)(row0 + r) * ldfb + c16 * 16, __builtin_amdgcn_readfirstlane(buf + ZB + seg * 1024));
@@ -441,7 +486,7 @@ MARF_DEV void wgrad_dma_body(const WgArgs& a, int chunk_id, int ob, char* smem) 
 #pragma unroll
             for (int r = 0; r < SP; r += 2) {
                 const int rr = r + (threadIdx.x >> 8);
-                bsum += P::tof(*reinterpret_cast<const u16*>(tz + swz(rr, c)));
+                bsum += P::tof(*reinterpret_cast<const u16*>(tz + (T16 ? t16_lds(rr, c, 16) : swz(rr, c))));
             }
         }
 #pragma unroll
@@ -450,14 +495,20 @@ MARF_DEV void wgrad_dma_body(const WgArgs& a, int chunk_id, int ob, char* smem) 
             typename P::frag af[RT], bf[CT];
 #pragma unroll
             for (int i = 0; i < RT; ++i) {
-                const u16* base = reinterpret_cast<const u16*>(tz + swz(r0, (wr * RT + i) * 32 + 16 * (g & 1) + 4 * p4));
-                i16x4 v[2] = {tr_read(base), tr_read(base + 4 * 256)};
+                const int c = (wr * RT + i) * 32 + 16 * (g & 1) + 4 * p4;
+                const u16* base = reinterpret_cast<const u16*>(tz + (T16 ? t16_lds(r0, c, 16) : swz(r0, c)));
+                const u16* base4 = T16 ? reinterpret_cast<const u16*>(tz + t16_lds(r0 + 4, c, 16)) : base + 4 * 256;
+                i16x4 v[2] = {tr_read(base), tr_read(base4)};
                 af[i] = *reinterpret_cast<typename P::frag*>(v);
             }
 #pragma unroll
             for (int j = 0; j < CT; ++j) {
-                const u16* base = reinterpret_cast<const u16*>(tf + foff<KF>(r0, (wc * CT + j) * 32 + 16 * (g & 1) + 4 * p4));
-                i16x4 v[2] = {tr_read(base), tr_read(base + 4 * KF)};
+                const int c = (wc * CT + j) * 32 + 16 * (g & 1) + 4 * p4;
+                // (F0: the recomputed feat_0 keeps its own row layout)
+                constexpr bool FT = T16 && !F0;
+                const u16* base = reinterpret_cast<const u16*>(tf + (FT ? t16_lds(r0, c, KF >> 4) : foff<KF>(r0, c)));
+                const u16* base4 = FT ? reinterpret_cast<const u16*>(tf + t16_lds(r0 + 4, c, KF >> 4)) : base + 4 * KF;
+                i16x4 v[2] = {tr_read(base), tr_read(base4)};
                 bf[j] = *reinterpret_cast<typename P::frag*>(v);
             }
 #pragma unroll
@@ -487,7 +538,7 @@ MARF_DEV void wgrad_dma_body(const WgArgs& a, int chunk_id, int ob, char* smem) 
     }
 }
 
-template <class P, int NBUF, int SP, int KF, bool F0 = false>
+template <class P, int NBUF, int SP, int KF, bool F0 = false, bool T16 = false>
 __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // (chunk, output block): wider layers (M, K multiples of 256, e.g. 512) split the output in
@@ -503,7 +554,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_dma(WgArgs a) {
         chunk_id = blockIdx.x % a.n_chunks;
         ob = blockIdx.x / a.n_chunks;
     }
-    wgrad_dma_body<P, NBUF, SP, KF, F0>(a, chunk_id, ob, smem);
+    wgrad_dma_body<P, NBUF, SP, KF, F0, T16>(a, chunk_id, ob, smem);
 }
 
 // Last layer (3 outputs): dW[c][k] = sum_px g[px][c] feat[px][k], db[c] = sum_px g[px][c].
@@ -624,7 +675,7 @@ template <class P, int NBUF, int SP, int KF>
 __global__ __launch_bounds__(512, 1) void k_wgrad_dma_layers(WgLayersArgs la) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int l = blockIdx.x / la.n_chunks, c = blockIdx.x - l * la.n_chunks;  // layer-major
-    wgrad_dma_body<P, NBUF, SP, KF>(la.a[l], c, 0, smem);
+    wgrad_dma_body<P, NBUF, SP, KF, false, true>(la.a[l], c, 0, smem);  // (the step kernel's T16 tensors)
 }
 
 struct WgRedJob {
@@ -731,7 +782,7 @@ static bool wgrad_dma_enabled() {
     return !(e && e[0] == '0');
 }
 
-template <class P, int KF, bool F0 = false>
+template <class P, int KF, bool F0 = false, bool T16 = false>
 static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
     a.n_chunks = n_chunks;
     a.n_oblk_c = (a.K + KF - 1) / KF;
@@ -739,10 +790,11 @@ static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
     constexpr int NBUF = KF == 256 ? WG_NBUF_H : F0 ? WG_NBUF_0 : WG_NBUF_96;  // ring depth within 160 KB of LDS
     const size_t lds = (size_t)NBUF * SP * (512 + KF * 2) + (KF == 256 ? 0 : 1024) + (F0 ? (9 * F0_PATCHES + 32 + (NBUF + 1) * SP * 2) * 4 : 0);
     {
-        hipError_t e = ensure_dynamic_lds((const void*)k_wgrad_dma<P, NBUF, SP, KF, F0>, lds);
+        hipError_t e = ensure_dynamic_lds((const void*)k_wgrad_dma<P, NBUF, SP, KF, F0, T16>, lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((k_wgrad_dma<P, NBUF, SP, KF, F0>), dim3(n_chunks * (a.M / 256) * a.n_oblk_c), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((k_wgrad_dma<P, NBUF, SP, KF, F0, T16>), dim3(n_chunks * (a.M / 256) * a.n_oblk_c), dim3(512), lds, s,
+                       a);
     return hipGetLastError();
 }
 
@@ -750,9 +802,10 @@ static hipError_t launch_wg_dma(WgArgs a, int n_chunks, hipStream_t s) {
 // 256x64 (2x1) or 128x64 (1x1).
 hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
                              int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s,
-                             const WgRange* rng) {
+                             const WgRange* rng, bool t16) {
     WgArgs a;
     memset(&a, 0, sizeof(a));
+    a.t16 = t16 ? 1 : 0;
     if (rng) {
         a.s_lo = rng->s_lo;
         a.s_len = rng->s_len;
@@ -784,17 +837,18 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
     const bool dma256 = dma && K % 256 == 0 && ldf % 8 == 0 && ldf >= K && S % WG_SPH == 0 && chunk % WG_SPH == 0,
                dma96 = dma && K == 96 && ldf == 96;
     if (rng && (dtype == 0 || !(dma256 || dma96))) return hipErrorInvalidValue;  // range mode: LDS-DMA kernel only
+    if (t16 && dtype == 0) return hipErrorInvalidValue;  // (T16: 16-bit tensors of the step kernel only)
     if (dtype == 1) {
-        if (dma256) return launch_wg_dma<PrecBF16, 256>(a, n_chunks, s);
-        if (dma96) return launch_wg_dma<PrecBF16, 96>(a, n_chunks, s);
+        if (dma256) return t16 ? launch_wg_dma<PrecBF16, 256, false, true>(a, n_chunks, s) : launch_wg_dma<PrecBF16, 256>(a, n_chunks, s);
+        if (dma96) return t16 ? launch_wg_dma<PrecBF16, 96, false, true>(a, n_chunks, s) : launch_wg_dma<PrecBF16, 96>(a, n_chunks, s);
         if (cfg == 0) return launch_wg<PrecBF16, 2, 4>(a, n_chunks, nr * nc, s);
         if (cfg == 3) return launch_wg<PrecBF16, 2, 2>(a, n_chunks, nr * nc, s);
         if (cfg == 1) return launch_wg<PrecBF16, 2, 1>(a, n_chunks, nr * nc, s);
         return launch_wg<PrecBF16, 1, 1>(a, n_chunks, nr * nc, s);
     }
     if (dtype == 2) {
-        if (dma256) return launch_wg_dma<PrecF16, 256>(a, n_chunks, s);
-        if (dma96) return launch_wg_dma<PrecF16, 96>(a, n_chunks, s);
+        if (dma256) return t16 ? launch_wg_dma<PrecF16, 256, false, true>(a, n_chunks, s) : launch_wg_dma<PrecF16, 256>(a, n_chunks, s);
+        if (dma96) return t16 ? launch_wg_dma<PrecF16, 96, false, true>(a, n_chunks, s) : launch_wg_dma<PrecF16, 96>(a, n_chunks, s);
         if (cfg == 0) return launch_wg<PrecF16, 2, 4>(a, n_chunks, nr * nc, s);
         if (cfg == 3) return launch_wg<PrecF16, 2, 2>(a, n_chunks, nr * nc, s);
         if (cfg == 1) return launch_wg<PrecF16, 2, 1>(a, n_chunks, nr * nc, s);
@@ -845,10 +899,11 @@ hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev&
     a.ldf = 96;
     a.M = M;
     a.K = K0;  // partial columns: 96, or the first 64 of the 96-wide stage
+    a.t16 = 1;  // dz_1 from the step kernel
     a.chunk = chunk;
     a.partial = partial;
     a.bpartial = bpartial;
-    return launch_wg_dma<PrecBF16, 96, true>(a, n_chunks, s);
+    return launch_wg_dma<PrecBF16, 96, true, true>(a, n_chunks, s);
 }
 
 // ---- the fused launch: hidden layers in one launch, layer 0 beside it on `s2`, one reduction launch
@@ -900,7 +955,7 @@ hipError_t marf_launch_wgrad_fused(const WgFusedLayer* layers, int n_layers, lon
                                                l0->bpartial, s2);
         else
             e = marf_launch_wgrad(1, l0->dz, l0->ldz, l0->feat, l0->ldf, S, l0->M, l0->K, chunk, n_chunks, l0->partial,
-                                  l0->bpartial, s2);
+                                  l0->bpartial, s2, nullptr, true);
         if (e != hipSuccess) return e;
         if ((e = hipEventRecord(join, s2)) != hipSuccess) return e;
     }
@@ -925,6 +980,7 @@ hipError_t marf_launch_wgrad_fused(const WgFusedLayer* layers, int n_layers, lon
         a.n_oblk_c = 1;
         a.partial = Ly.partial;
         a.bpartial = Ly.bpartial;
+        a.t16 = 1;
     }
     if (nh) {
         const size_t lds = (size_t)WG_NBUF_H * WG_SPH * (512 + 256 * 2);
