@@ -24,13 +24,13 @@ DMA_ASM = ('asm volatile("s_mov_b32 %0, m0\\n\\ts_mov_b32 m0, %2\\n\\ts_nop 0\\n
            '                     : "=&s"(keep)\n'
            '                     : "v"(va), "s"(m), "n"((j & 3) * 1024)\n'
            '                     : "memory");')
-SAVE = ("        s2_st16o<64 * rt>(row0, contig(f0));\n"
-        "        s2_st16o<64 * rt + 32>(row0, contig(f1));\n"
+SAVE = ("        s2_st16o<0>(blk, contig(f0));\n"
+        "        s2_st16o<1024>(blk, contig(f1));\n"
         "        st_cur += 2;\n")
 
 PATCHES = {
     "nodma": [("marf_step2.hip", DMA_ASM, "(void)va; (void)m; keep = 0; (void)keep;")],
-    "nosave": [("marf_step2.hip", SAVE, "        (void)row0; (void)f0; (void)f1; (void)contig;\n")],
+    "nosave": [("marf_step2.hip", SAVE, "        (void)blk; (void)f0; (void)f1; (void)contig;\n")],
 }
 PATCHES["nodma_nosave"] = PATCHES["nodma"] + PATCHES["nosave"]
 # cache-policy variants (correct results, same bits): the weight-ring DMA and / or the saved-tensor
