@@ -5,6 +5,7 @@ free of diagnostic switches):  python tools/ab_variant.py NAME [NAME ...]  ->  l
                  held): what the step kernel costs without streaming its weight program
   nosave         k_step2 without its saved-tensor stores (feat_l, dz_l) and their vmcnt accounting
   nodma_nosave   both
+  tilenosave     the tile kernels without their saved-tile stores (C5)
 
   dmant / stnt / stsc1 / dmant_stnt   cache-policy bits on the weight DMA / the saved-tensor stores
                  (correct results, the same bits)
@@ -33,6 +34,9 @@ PATCHES = {
     "nosave": [("marf_step2.hip", SAVE, "        (void)blk; (void)f0; (void)f1; (void)contig;\n")],
 }
 PATCHES["nodma_nosave"] = PATCHES["nodma"] + PATCHES["nosave"]
+# the tile kernels (k_mlp_step / k_mlp_fwd / k_mlp_bwd) without their saved-tile stores: what the
+# stores and the loads queued behind them (vmcnt retires in issue order) cost C5
+PATCHES["tilenosave"] = [("marf_gemm.h", "    if (st.active) st.flush(act);\n}", "    (void)st;\n}")]
 # cache-policy variants (correct results, same bits): the weight-ring DMA and / or the saved-tensor
 # stores with the nt (streaming) or sc1 (write-through) policy bits
 DMA_OP = "global_load_lds_dwordx4 %1, off offset:%3"
