@@ -47,6 +47,7 @@ static inline long long rup(long long x, long long m) { return (x + m - 1) / m *
 struct Step2NetPlan {
     int variant;           // -1: not available for this net; 0: bf16 (8 waves); 1: split bf16 (4 waves);
                            // 2: bf16 on 4 waves (diagnostic)
+    bool dz;               // variant 1 with the dgrad's dz split too (MARF_STEP2_DZ=1 at net creation)
     int NW, NS, HM, MAXR, NMW, slot, nk0, nta, n_stages, nbias, Kl, ldf0;
     int PX, TPX;           // pixels per wave, pixel slots per block tile
     int nslot;             // weight-ring slots in LDS
@@ -128,7 +129,11 @@ static void plan_step2_net(marf_net* n, long long pixels_hint) {
     }
     q.NW = q.variant == 0 ? 8 : 4;
     q.nslot = 3;
-    q.NS = q.variant == 1 ? 2 : 1;  // pixel sets per dgrad pass (S2Cfg::NS)
+    {  // the split recipe with dz split in the dgrad too (k_step2's DZ; numerics option)
+        const char* e = getenv("MARF_STEP2_DZ");
+        q.dz = q.variant == 1 && e && e[0] == '1';
+    }
+    q.NS = q.variant == 1 && !q.dz ? 2 : 1;  // pixel sets per dgrad pass (S2Cfg::NS)
     q.PX = 32;
     q.TPX = 32 * q.NW;
     q.MAXR = 4;
@@ -1074,7 +1079,7 @@ static hipError_t launch_s2(const marf_net* n, const Step2Args& a, int grid, hip
     bool full = q.variant == 1 && q.nk0 >= 1 && q.r0 == std::max(1, std::min(8, 16 / q.nk0)) && q.Kl == 256;
     for (int l = 0; l < n->n_layers - 1; ++l) full = full && n->Mp[l] == 256;
     if (const char* e = getenv("MARF_STEP2_GENERIC")) full = full && e[0] != '1';  // (A/B: the generic kernel)
-    return marf_launch_step2(a, q.variant, grid, s, full ? q.nk0 : 0);
+    return marf_launch_step2(a, q.variant, grid, s, full ? q.nk0 : 0, q.dz);
 }
 
 static int step2_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,

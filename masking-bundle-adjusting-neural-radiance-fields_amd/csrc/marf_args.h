@@ -190,7 +190,7 @@ hipError_t marf_launch_mlp_step(const marf::StepArgs& a, int dtype, int TP, int 
 hipError_t marf_launch_c2f_weights(const marf::C2fDev& c, int L, float* out, hipStream_t s,
                                    const int* csrc = nullptr, int* cdst = nullptr, int cn = 0);
 hipError_t marf_launch_loss_final(const double* part, int n, float* out, const float* denom_override, hipStream_t s);
-hipError_t marf_launch_step2(const marf::Step2Args& a, int variant, int grid, hipStream_t s, int full_nk0);
+hipError_t marf_launch_step2(const marf::Step2Args& a, int variant, int grid, hipStream_t s, int full_nk0, bool dz = false);
 hipError_t marf_launch_pack2(const float* params, void* prog, float* bias_out, int* kmap, const marf::Pack2Args& a,
                              hipStream_t s);
 hipError_t marf_launch_edge_map(const float* in, double* out, int n_img, int H, int W, hipStream_t s);

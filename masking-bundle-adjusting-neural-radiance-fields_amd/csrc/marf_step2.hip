@@ -133,7 +133,7 @@ MARF_DEV void s2_split8(const float* x, S2Frag& hi, S2Frag& lo) {
     } while (0)
 #endif
 
-template <int HM, bool SPLIT, int NW, int MAXR>
+template <int HM, bool SPLIT, int NW, int MAXR, bool DZ = false>
 struct S2Cfg {
     static constexpr int NKH = HM / 16;                    // k-steps of a hidden-width operand
     static constexpr int NRT = HM / 32;                    // row tiles of a hidden-width output
@@ -144,7 +144,8 @@ struct S2Cfg {
     // pixel sets (tiles) whose dgrad shares each weight stage: the split recipe's dgrad operands are
     // bf16 hi only, so at one wave per SIMD two 32-pixel sets fit the register file there (the
     // forward's hi + lo activations do not); the 8-wave plain variant has 256 registers per wave
-    static constexpr int NS = SPLIT ? 2 : 1;
+    // (DZ: the dgrad operand dz split hi + lo as well: one set, its lo in the lo arrays)
+    static constexpr int NS = SPLIT && !DZ ? 2 : 1;
     static constexpr int NK0 = 9;                          // max layer-0 k-steps (L <= 32)
     static constexpr int NTA = 5;                          // max adjoint row tiles (L <= 39)
     static constexpr int TPX = 32 * NW;                    // pixel slots per block tile
@@ -157,9 +158,14 @@ struct S2Cfg {
 // run time); > 0 = a full-width net (every hidden layer HM wide) with NK0F layer-0 k-steps and NTAF
 // adjoint row tiles, whose layer-0 stages, GEMM lengths and row-tile counts are compile-time (no
 // live-k-step branches; 10.4 -> 9.5 ms at C3, profiles/r4r)
-template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0, int NTAF = 0>
-__global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
-    typedef S2Cfg<HM, SPLIT, NW, MAXR> C;
+// DZ (split recipe, opt-in MARF_STEP2_DZ=1): the hidden dgrad GEMMs also split their dz operand,
+// W_hi^T dz_hi + W_lo^T dz_hi + W_hi^T dz_lo (the forward's three terms), one pixel set per dgrad
+// pass; dz_1 (the layer-0 adjoint's operand) and the saved dz stay bf16 hi.  DESIGN.md §4: the
+// recipe whose emulation reaches fp32's basin rate.
+template <int HM, bool SPLIT, int NW, int MAXR, int NK0F, int NTAF, bool DZ>
+__device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Args& a) {
+    typedef S2Cfg<HM, SPLIT, NW, MAXR, DZ> C;
+    constexpr bool SDZ = SPLIT && DZ;
     constexpr int NKH = C::NKH, NRT = C::NRT, NS = C::NS;
     constexpr bool FIX = NK0F > 0;
     static_assert(NK0F <= C::NK0, "layer-0 k-steps");
@@ -462,6 +468,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
     };
     typedef std::integral_constant<int, SPLIT ? 1 : 0> MFt;
     typedef std::integral_constant<int, SPLIT ? 2 : 0> MBt;
+    // the hidden dgrad GEMMs: the forward's split mode when dz is split too (SDZ), else MBt
+    typedef std::integral_constant<int, SDZ ? 1 : (SPLIT ? 2 : 0)> MDt;
     typedef std::integral_constant<int, NKH> NKHt;
     typedef std::integral_constant<int, C::NK0> NK0t;
     // layer 0's GEMM length: compile-time NK0F (every k-step live) or NK0 with a run-time count
@@ -639,6 +647,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             uint32_t w;
             asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(es.vp), "v"(x));
             es.hw[e >> 1] = w;
+            if constexpr (SDZ) es.lw[e >> 1] = s2_pk(es.vp - s2_lo16(w), x - s2_hi16(w));
         } else {
             es.vp = x;
         }
@@ -653,12 +662,17 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
             const float x0 = __int_as_float(__builtin_amdgcn_sbfe((int)es.mw, b0, 1) & __float_as_int(pa[2 * q]));
             const float x1 = __int_as_float(__builtin_amdgcn_sbfe((int)es.mw, b1, 1) & __float_as_int(pa[2 * q + 1]));
             es.hw[q] = s2_pk(x0, x1);
+            if constexpr (SDZ) es.lw[q] = s2_pk(x0 - s2_lo16(es.hw[q]), x1 - s2_hi16(es.hw[q]));
         });
     };
     auto bfinish = [&](EpSt& es, S2Frag* O, auto rtc, u16* row0) {
         constexpr int rt = decltype(rtc)::value;
         O[2 * rt].u = make_uint4(es.hw[0], es.hw[1], es.hw[2], es.hw[3]);
         O[2 * rt + 1].u = make_uint4(es.hw[4], es.hw[5], es.hw[6], es.hw[7]);
+        if constexpr (SDZ) {  // (one pixel set: its lo output in the lo array)
+            Ol[2 * rt].u = make_uint4(es.lw[0], es.lw[1], es.lw[2], es.lw[3]);
+            Ol[2 * rt + 1].u = make_uint4(es.lw[4], es.lw[5], es.lw[6], es.lw[7]);
+        }
         store_rt(row0, rtc, O[2 * rt], O[2 * rt + 1]);
     };
     const float pi_f = 3.14159265358979323846f;
@@ -1044,8 +1058,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 }
             });
 #pragma unroll
-            for (int k = 0; k < NKH; ++k)
+            for (int k = 0; k < NKH; ++k) {
                 s2_sfor<NS>([&](auto sc) { Dh[decltype(sc)::value][k] = Do[decltype(sc)::value][k]; });
+                if constexpr (SDZ) Bl[k] = Ol[k];
+            }
         }
         // ---- hidden dgrad chain l = nl-2 .. 1
         for (int l = nl - 2; l >= 1; --l) {
@@ -1067,12 +1083,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                         cur = (f32x16){};
                         if constexpr (i == 0) {
                             S2T_BEGIN(9);
-                            gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), nohook, std::integral_constant<bool, s == 0>());
+                            gemm(cur, slot, Dh[s], SDZ ? Bl : Dh[s], NKH, MDt(), NKHt(), nohook, std::integral_constant<bool, s == 0>());
                             S2T_END(9);
                         } else {
                             eb.mw = mks_b(sp)[(lmask * C::NMW + (rp >> 1)) * 64 + lane];
                             S2T_BEGIN(9);
-                            gemm(cur, slot, Dh[s], Dh[s], NKH, MBt(), NKHt(), [&](auto ksc, auto pc) {
+                            gemm(cur, slot, Dh[s], SDZ ? Bl : Dh[s], NKH, MDt(), NKHt(), [&](auto ksc, auto pc) {
                                 if constexpr (decltype(pc)::value == 0) bstep(eb, prv, ksc, std::integral_constant<int, rp>());
                             }, std::integral_constant<bool, s == 0>());
                             S2T_END(9);
@@ -1095,8 +1111,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
                 }
             });
 #pragma unroll
-            for (int k = 0; k < NKH; ++k)
+            for (int k = 0; k < NKH; ++k) {
                 s2_sfor<NS>([&](auto sc) { Dh[decltype(sc)::value][k] = Do[decltype(sc)::value][k]; });
+                if constexpr (SDZ) Bl[k] = Ol[k];
+            }
         }
         // ---- layer-0 dgrad + posenc adjoint: row (tile t, register r) = slot 16 t + r of the
         //      lane's coordinate: slot 2k = sin band k, 2k + 1 = cos band k, 2L = the raw coordinate.
@@ -1274,6 +1292,18 @@ MARF_DEV int s2_l0_adj_feature(int t, int rho, int L) {
     const int k = sl >> 1;
     return 2 + 2 * hh * L + ((sl & 1) ? L : 0) + k;
 }
+
+template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0, int NTAF = 0>
+__global__ __launch_bounds__(NW * 64, NW / 4) void k_step2(Step2Args a) {
+    k_step2_body<HM, SPLIT, NW, MAXR, NK0F, NTAF, false>(a);
+}
+
+// the split recipe with dz split in the dgrad too (opt-in: MARF_STEP2_DZ=1)
+template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0, int NTAF = 0>
+__global__ __launch_bounds__(NW * 64, NW / 4) void k_step2dz(Step2Args a) {
+    k_step2_body<HM, SPLIT, NW, MAXR, NK0F, NTAF, true>(a);
+}
+
 // permuted k (hidden operand from an accumulator): k-step ks, lane half hh, element j
 MARF_DEV int s2_kperm(int ks, int hh, int j) { return 16 * ks + 8 * (j >> 2) + 4 * hh + (j & 3); }
 
@@ -1394,11 +1424,17 @@ __global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog
 
 using namespace marf;
 
-template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0, int NTAF = 0>
+template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0, int NTAF = 0, bool DZ = false>
 static hipError_t launch_step2_t(const Step2Args& a, int grid, hipStream_t s) {
-    hipError_t e = ensure_dynamic_lds((const void*)k_step2<HM, SPLIT, NW, MAXR, NK0F, NTAF>, (size_t)a.lds_total);
+    const void* k;
+    if constexpr (DZ) k = (const void*)k_step2dz<HM, SPLIT, NW, MAXR, NK0F, NTAF>;
+    else k = (const void*)k_step2<HM, SPLIT, NW, MAXR, NK0F, NTAF>;
+    hipError_t e = ensure_dynamic_lds(k, (size_t)a.lds_total);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_step2<HM, SPLIT, NW, MAXR, NK0F, NTAF>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
+    if constexpr (DZ)
+        hipLaunchKernelGGL((k_step2dz<HM, SPLIT, NW, MAXR, NK0F, NTAF>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
+    else
+        hipLaunchKernelGGL((k_step2<HM, SPLIT, NW, MAXR, NK0F, NTAF>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
     return hipGetLastError();
 }
 
@@ -1407,7 +1443,13 @@ static hipError_t launch_step2_t(const Step2Args& a, int grid, hipStream_t s) {
 // full_nk0: a full-width net's layer-0 k-step count (its r0 and row-tile counts follow from it; see
 // k_step2's NK0F), or 0 for the generic instantiation; the compile-time instantiations cover
 // (nk0, nta) = (5, 3): L = 16; (5, 2): L = 13..15; (4, 2): L = 9..12; (3, 2): L = 8
-hipError_t marf_launch_step2(const Step2Args& a, int variant, int grid, hipStream_t s, int full_nk0) {
+// dz: the split recipe with the dgrad's dz split too (k_step2's DZ; L = 8 and 16 instantiated)
+hipError_t marf_launch_step2(const Step2Args& a, int variant, int grid, hipStream_t s, int full_nk0, bool dz) {
+    if (variant == 1 && dz) {
+        if (full_nk0 == 5 && a.nta == 3) return launch_step2_t<256, true, 4, 4, 5, 3, true>(a, grid, s);
+        if (full_nk0 == 3 && a.nta == 2) return launch_step2_t<256, true, 4, 4, 3, 2, true>(a, grid, s);
+        return launch_step2_t<256, true, 4, 4, 0, 0, true>(a, grid, s);
+    }
     switch (variant) {
         case 0: return launch_step2_t<256, false, 8, 4>(a, grid, s);
         case 1:
