@@ -1055,6 +1055,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                         constexpr int s = decltype(sc)::value;
                         Do[s][2 * rt].u = Do[s][2 * rt + 1].u = make_uint4(0, 0, 0, 0);
                     });
+                    if constexpr (SDZ) Ol[2 * rt].u = Ol[2 * rt + 1].u = make_uint4(0, 0, 0, 0);
                 }
             });
 #pragma unroll
@@ -1108,6 +1109,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                         constexpr int s = decltype(sc)::value;
                         Do[s][2 * rt].u = Do[s][2 * rt + 1].u = make_uint4(0, 0, 0, 0);
                     });
+                    if constexpr (SDZ) Ol[2 * rt].u = Ol[2 * rt + 1].u = make_uint4(0, 0, 0, 0);
                 }
             });
 #pragma unroll
