@@ -1,6 +1,6 @@
 """Throughput of the planar bundle-adjustment training step on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c1|c5] [--precision bf16x3|bf16|fp16|fp32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c1|c5] [--precision bf16x3|fp16x2|bf16|fp16|fp32]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -34,6 +34,7 @@ PEAK_BF16 = 2.5e15   # dense bf16 MFMA, MI355X_MICROARCH.md
 PEAK_FP32 = 157.3e12  # fp32 MFMA = vector rate
 PEAK_HBM = 8.0e12
 RECIPES = {"bf16x3": "bf16x3 recipe (split-bf16 hi+lo MFMA operands, fp32 accumulate; seed-3 parity)",
+           "fp16x2": "fp16x2 recipe (fp16 hi+lo weights x fp16 activations forward, split-bf16 dgrad; fp32 accumulate)",
            "bf16": "plain bf16 MFMA (fp32 accumulate)", "fp16": "plain fp16 MFMA (fp32 accumulate)", "fp32": "fp32"}
 
 CONFIGS = {
@@ -82,7 +83,8 @@ def pmc_traffic(cfg, precision, kernel, symbol_prefix):
             return None
         if symbol_prefix and not e["symbol"].startswith(symbol_prefix):
             return None
-        return e["hbm_read_bytes"] + e["hbm_write_bytes"], f"{d['source']}; {e['symbol']}; source hash {d['source_hash']}"
+        return (e["hbm_read_bytes"] + e["hbm_write_bytes"], f"{d['source']}; {e['symbol']}; source hash {d['source_hash']}",
+                {k: e.get(k) for k in ("mfma_busy", "valu_per_mfma", "SQ_INSTS_VMEM_RD")})
     except (OSError, KeyError, ValueError, TypeError):
         return None
 
@@ -215,7 +217,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=list(CONFIGS))
-    ap.add_argument("--precision", default=None, choices=["bf16x3", "bf16", "fp16", "fp32"],
+    ap.add_argument("--precision", default=None, choices=["bf16x3", "fp16x2", "bf16", "fp16", "fp32"],
                     help="default bf16x3 (the seed-3 parity recipe); c5's 512-wide layers: bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2f", action="store_true", help="barf_c2f None (BASELINE config 5: c2f on vs off)")
@@ -225,7 +227,8 @@ def main():
     ap.add_argument("--no-render", action="store_true",
                     help="skip the forward-only render rate (PMC passes: its launches share the step kernel's name)")
     ap.add_argument("--graph", action="store_true",
-                    help="replay forward + loss + backward as one captured HIP graph (Model.captured_step); "
+                    help="replay the whole iteration (forward, loss, backward, Adam, progress, fix_first) as one "
+                         "captured HIP graph (Model.captured_step); "
                          "the per-kernel times and the roofline then come from eager steps")
     ap.add_argument("--launch-check", action="store_true",
                     help="set up the ranks and print the JSON line's world size / backend only (no GPU work)")
@@ -300,12 +303,14 @@ def main():
 
     def step(eager=False):
         if args.graph and not eager:
+            # the whole iteration replayed: forward, loss, backward, Adam, progress, fix_first
             v, loss = m.captured_step(var)
-        else:
-            m.optim.zero_grad()
-            v = graph.forward(var, mode="train")
-            loss = m._loss_sum(graph.compute_loss(v, mode="train"))  # summarize_loss without host syncs
-            loss.all.backward()
+            graph.neural_image.progress.data.fill_(0.2)  # keep c2f partially on
+            return loss
+        m.optim.zero_grad()
+        v = graph.forward(var, mode="train")
+        loss = m._loss_sum(graph.compute_loss(v, mode="train"))  # summarize_loss without host syncs
+        loss.all.backward()
         m.all_reduce_grads()
         m.optim.step()
         graph.neural_image.progress.data.fill_(0.2)  # keep c2f partially on
@@ -385,7 +390,7 @@ def main():
     Kp0 = (dims[0] + 31) // 32 * 32
     S = (b1 - b0) * ((h * w + 127) // 128 * 128)
     sum_mac = sum(a * b for a, b in zip(dims[:-1], dims[1:]))
-    fwd_mult, bwd_mult = (3, 2) if args.precision == "bf16x3" else (1, 1)
+    fwd_mult, bwd_mult = {"bf16x3": (3, 2), "fp16x2": (2, 2)}.get(args.precision, (1, 1))
     kflops = {  # (algorithmic, MFMA-issued) FLOPs per launch
         # fused step: forward + dgrad chain (incl. layer 0, for the warp gradient) + last-layer wgrad
         "mlp_step": (px_local * (4 * sum_mac + 6 * dims[-2]),
@@ -418,7 +423,11 @@ def main():
                 "mfma_tflops": issued / avg_s / 1e12, "mfma_frac": issued / avg_s / peak,
                 "algorithmic_bytes_per_launch": alg_bytes, "design_bytes_per_launch": design,
                 "traffic_ratio": (tr[0] / alg_bytes) if (tr and alg_bytes) else None,
-                "traffic_source": tr[1] if tr else None}
+                "traffic_source": tr[1] if tr else None,
+                # matrix-core counters of the same kernel on the same library (PMC pass, null otherwise)
+                "mfma_busy": tr[2].get("mfma_busy") if tr else None,
+                "valu_per_mfma": tr[2].get("valu_per_mfma") if tr else None,
+                "vmem_rd_insts_per_launch": tr[2].get("SQ_INSTS_VMEM_RD") if tr else None}
     prologue = prologue_rate(graph, var, L, opt.barf_c2f) if world == 1 or rank == 0 else None
     ms = elapsed / args.steps * 1e3
     value = world * px_local / (elapsed / args.steps)

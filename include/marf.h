@@ -17,7 +17,8 @@
  *     returns a thread-local message for the last failure.
  *   - float32 everywhere in the interface; dtype selects the internal MLP arithmetic
  *     (MARF_FP32 = exact fp32 MFMA, MARF_BF16 = bf16 MFMA with fp32 accumulation, MARF_BF16X3 = split
- *     bf16, MARF_FP16 = fp16 MFMA with fp32 accumulation).
+ *     bf16, MARF_FP16 = fp16 MFMA with fp32 accumulation, MARF_FP16X2 = split fp16 forward + split
+ *     bf16 dgrad).
  */
 #ifndef MARF_H
 #define MARF_H
@@ -42,6 +43,10 @@ extern "C" {
 
 #define MARF_FP16 3   /* fp16 MFMA (v_mfma_f32_32x32x16_f16, fp32 accumulation): weights, activations, dz and the
                          saved tensors in IEEE binary16 (11 significant bits); the bf16 rate */
+#define MARF_FP16X2 4 /* split fp16 forward: weights as fp16 hi + lo pairs, forward activations single fp16
+                         (hi*a + lo*a: 2 MFMAs per MAC), the dgrad, dz and saved tensors as MARF_BF16X3;
+                         full-width nets (every hidden layer 256 wide, <= 5 layers, L <= 32, no skip);
+                         fused step and marf_render only */
 
 #define MARF_GEO_GRID 0   /* pixels of the centre crop, warped by a per-patch homography */
 #define MARF_GEO_COORDS 1 /* explicit [n][2] coordinates (one point set) */
@@ -229,6 +234,14 @@ int marf_erode_rect(const float* d_img, int n_img, int H, int W, int kh, int kw,
  * d_grad_scale: optional device scalar multiplying the gradient (NULL = 1). */
 int marf_adam_step(float* d_p, const float* d_g, float* d_m, float* d_v, long long n, double lr, double beta1,
                    double beta2, double eps, long long step, const float* d_grad_scale, void* stream);
+/* The same update with the step's scalars read on the device, so a captured training iteration
+ * (Model.captured_step) replays it without host values: marf_adam_schedule fills h_out[2 i],
+ * h_out[2 i + 1] with step_size = lr / (1 - beta1^k) and sqrt(1 - beta2^k) for k = first_step + i,
+ * exactly as marf_adam_step computes them (host only); marf_adam_step_sched reads row *d_index of
+ * that table (uploaded by the caller) on the stream. */
+int marf_adam_schedule(double lr, double beta1, double beta2, long long first_step, long long count, float* h_out);
+int marf_adam_step_sched(float* d_p, const float* d_g, float* d_m, float* d_v, long long n, double beta1, double beta2,
+                         double eps, const float* d_sched, const int* d_index, const float* d_grad_scale, void* stream);
 
 /* ---- Profiling: HIP events recorded around each kernel on its launch stream (off by default).
  * marf_profile_read drains the recorded pairs (synchronising on them) and returns, per kernel

@@ -64,36 +64,70 @@ def build(force=False, verbose=True, stamps=False):
     return _compile(LIB, [], verbose)
 
 
+OBJ_CACHE = os.path.join(HERE, "build", "obj")  # compiled translation units, keyed by their inputs
+
+
+def _unit_key(src, cflags):
+    """sha1 of one translation unit's compile: hipcc flags (less the library hash, which only
+    marf_abi.hip embeds), its source and every header under csrc/ and include/."""
+    h = hashlib.sha1()
+    flags = [f for f in cflags if not f.startswith("-DMARF_SOURCE_HASH") or src == "marf_abi.hip"]
+    h.update(" ".join(flags).encode())
+    deps = [os.path.join(HERE, "csrc", src)] + sorted(glob.glob(os.path.join(HERE, "csrc", "*.h")) +
+                                                      glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for d in deps:
+        h.update(os.path.relpath(d, ROOT).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def _compile(lib_path, extra, verbose):
-    """One hipcc process per translation unit (in parallel), then one link."""
+    """One hipcc process per translation unit (in parallel; units whose inputs are unchanged come
+    from build/obj), then one link."""
+    import shutil
     import tempfile
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     os.makedirs(os.path.dirname(lib_path), exist_ok=True)
+    os.makedirs(OBJ_CACHE, exist_ok=True)
     tmp = f"{lib_path}.tmp.{os.getpid()}"  # per process: concurrent builders never share a file
     if verbose:
         print("[marf] building", lib_path, flush=True)
     jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
     with tempfile.TemporaryDirectory() as td:
-        objs, procs, logs = [], [], []
-        cflags = [f for f in FLAGS if f != "-shared"] + [f'-DMARF_SOURCE_HASH="{source_hash()}"']
+        objs, procs, logs, cached = [], [], [], []
+        cflags = [f for f in FLAGS if f != "-shared"] + [f'-DMARF_SOURCE_HASH="{source_hash()}"'] + list(extra)
         for src in SOURCES:
+            key = _unit_key(src, cflags)
+            keep = os.path.join(OBJ_CACHE, f"{src[:-4]}-{key}.o")
+            cached.append(keep)
             obj = os.path.join(td, src.replace(".hip", ".o"))
             objs.append(obj)
+            if os.path.exists(keep):
+                shutil.copyfile(keep, obj)
+                procs.append(None)
+                logs.append(None)
+                continue
             # compiler output to a file, not a pipe: a pipe nobody drains blocks a verbose compile
             log = open(obj + ".log", "w+")
             logs.append(log)
-            procs.append(subprocess.Popen([hipcc] + cflags + extra + ["-c", os.path.join(HERE, "csrc", src), "-o", obj],
+            procs.append(subprocess.Popen([hipcc] + cflags + ["-c", os.path.join(HERE, "csrc", src), "-o", obj],
                                           stdout=log, stderr=subprocess.STDOUT))
-            while sum(p.poll() is None for p in procs) >= jobs:
-                procs[[p.poll() is None for p in procs].index(True)].wait()
+            while sum(p is not None and p.poll() is None for p in procs) >= jobs:
+                procs[[p is not None and p.poll() is None for p in procs].index(True)].wait()
         errs = []
-        for src, p, log in zip(SOURCES, procs, logs):
+        for src, p, log, obj, keep in zip(SOURCES, procs, logs, objs, cached):
+            if p is None:
+                continue
             p.wait()
             log.seek(0)
             out = log.read()
             log.close()
             if p.returncode != 0:
                 errs.append(f"{src}:\n{out}")
+            else:
+                shutil.copyfile(obj, keep + f".tmp.{os.getpid()}")
+                os.replace(keep + f".tmp.{os.getpid()}", keep)
         if errs:
             raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
         r = subprocess.run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", tmp],

@@ -46,7 +46,8 @@ static inline long long rup(long long x, long long m) { return (x + m - 1) / m *
 // step2 plan (the pixel-per-wave fused step, marf_step2.hip), filled by plan_step2_net
 struct Step2NetPlan {
     int variant;           // -1: not available for this net; 0: bf16 (8 waves); 1: split bf16 (4 waves);
-                           // 2: bf16 on 4 waves (diagnostic)
+                           // 2: bf16 on 4 waves (diagnostic); 3: fp16x2 (fp16 forward of two pixel sets
+                           // per stage, split-bf16 dgrad; 4 waves, compile-time layer 0 only)
     bool dz;               // variant 1 with the dgrad's dz split too (MARF_STEP2_DZ=1 at net creation)
     int NW, NS, HM, MAXR, NMW, slot, nk0, nta, n_stages, nbias, Kl, ldf0;
     int PX, TPX;           // pixels per wave, pixel slots per block tile
@@ -96,6 +97,9 @@ static void parse_diag(marf_net* n) {
     }
 }
 
+// the split recipes: every path runs k_step2's weight program (no tile-kernel arithmetic for them)
+static bool split_recipe(int dtype) { return dtype == MARF_BF16X3 || dtype == MARF_FP16X2; }
+
 static bool step2_env_enabled() {
     const char* e = getenv("MARF_STEP2");  // plain bf16 on the pixel-per-wave kernel: opt-in ("1")
     return e && e[0] == '1';
@@ -119,9 +123,9 @@ static void plan_step2_net(marf_net* n, long long pixels_hint) {
         if (n->Mp[l] > 256) return;
     // decided once, here: the split recipe always runs this kernel; plain bf16 only on request
     // (MARF_STEP2=1 at net creation), otherwise it runs the tile kernel and needs no program
-    if (n->dtype != MARF_BF16X3 && !step2_env_enabled()) return;
+    if (!split_recipe(n->dtype) && !step2_env_enabled()) return;
     q.HM = 256;
-    q.variant = n->dtype == MARF_BF16X3 ? 1 : 0;
+    q.variant = n->dtype == MARF_BF16X3 ? 1 : (n->dtype == MARF_FP16X2 ? 3 : 0);
     (void)pixels_hint;  // (kernel choice by size: none left to make)
     {
         const char* e = getenv("MARF_STEP2_NW4");  // diagnostic: plain bf16 on 4 waves per block
@@ -133,12 +137,12 @@ static void plan_step2_net(marf_net* n, long long pixels_hint) {
         const char* e = getenv("MARF_STEP2_DZ");
         q.dz = q.variant == 1 && e && e[0] == '1';
     }
-    q.NS = q.variant == 1 && !q.dz ? 2 : 1;  // pixel sets per dgrad pass (S2Cfg::NS)
+    q.NS = (q.variant == 1 && !q.dz) || q.variant == 3 ? 2 : 1;  // pixel sets per dgrad pass (S2Cfg::NS)
     q.PX = 32;
     q.TPX = 32 * q.NW;
     q.MAXR = 4;
     q.NMW = q.HM / 64;
-    q.slot = (q.HM / 16) * 1024 * (q.variant == 1 ? 2 : 1);
+    q.slot = (q.HM / 16) * 1024 * (q.variant == 1 || q.variant == 3 ? 2 : 1);
     q.nk0 = (n->L + 3) / 4 + 1;
     q.nk0w = q.nk0;
     q.nta = (2 * n->L + 1 + 15) / 16;
@@ -165,6 +169,12 @@ static void plan_step2_net(marf_net* n, long long pixels_hint) {
     q.bias_off = q.prog_off + (size_t)st * q.slot;
     q.kmap_off = rup((long long)(q.bias_off + (size_t)q.nbias * 4), 256);
     q.end_off = rup((long long)(q.kmap_off + (size_t)n->D * 4), 256);
+    if (q.variant == 3) {  // fp16x2: full-width nets with a compile-time layer-0 instantiation only
+        bool full = q.Kl == 256 && nl == 5 && q.r0 == std::max(1, std::min(8, 16 / q.nk0)) &&
+                    ((q.nk0 == 5 && (q.nta == 3 || q.nta == 2)) || (q.nk0 == 4 && q.nta == 2) || (q.nk0 == 3 && q.nta == 2));
+        for (int l = 0; l < nl - 1; ++l) full = full && n->Mp[l] == 256;
+        if (!full) q.variant = -1;
+    }
 }
 
 extern "C" {
@@ -369,7 +379,7 @@ int marf_net_create_skip(int n_layers, const int* dims, int L, int dtype, long l
     *out = nullptr;
     if (n_layers < 2 || n_layers > MARF_MAX_LAYERS)
         return fail(MARF_ERR_UNSUPPORTED, "net_create: n_layers=%d (supported 2..%d)", n_layers, MARF_MAX_LAYERS);
-    if (dtype != MARF_FP32 && dtype != MARF_BF16 && dtype != MARF_BF16X3 && dtype != MARF_FP16)
+    if (dtype != MARF_FP32 && dtype != MARF_BF16 && dtype != MARF_BF16X3 && dtype != MARF_FP16 && dtype != MARF_FP16X2)
         return fail(MARF_ERR_INVALID, "net_create: dtype %d", dtype);
     if (L < 0 || L > 32) return fail(MARF_ERR_UNSUPPORTED, "net_create: L=%d (supported 0..32)", L);
     int D = L > 0 ? 2 + 4 * L : 2;
@@ -452,9 +462,15 @@ int marf_net_create_skip(int n_layers, const int* dims, int L, int dtype, long l
             n->lds_step = std::max(act8, df8) + dsk8;
         }
     }
-    if (n->lds_bwd > 160 * 1024) {
+    // the 4-wave tile kernels' static __shared__ beside the dynamic tile (k_mlp_step: wsh, red, red9,
+    // gl, gT, lsum, bsh; the separate forward / backward kernels hold less): checked here, so a shape
+    // whose step would fail ensure_dynamic_lds at launch is refused at creation instead
+    const size_t static4 = 128 + (size_t)std::max(4 * 64, 2 * n->TP) * 2 * 4 + 4 * 9 * 4 + (size_t)n->TP * 16 +
+                           8 * (size_t)n->TP * n->elem + 2 * (size_t)n->TP * 4 + 16 + 512;
+    if (n->lds_bwd + static4 > 160 * 1024) {
         delete n;
-        return fail(MARF_ERR_UNSUPPORTED, "net_create: tile does not fit LDS");
+        return fail(MARF_ERR_UNSUPPORTED, "net_create: tile does not fit LDS (%zu B dynamic + %zu B static)", n->lds_bwd,
+                    static4);
     }
     long long off = 0;
     size_t boff = 0;
@@ -483,6 +499,11 @@ int marf_net_create_skip(int n_layers, const int* dims, int L, int dtype, long l
         n->pipe_piece = e && *e ? atoi(e) : 0;
     }
     if (n->s2.variant >= 0) n->packed_bytes = n->s2.end_off;
+    if (dtype == MARF_FP16X2 && n->s2.variant < 0) {
+        delete n;
+        return fail(MARF_ERR_UNSUPPORTED,
+                    "net_create: fp16x2 needs 5 layers, every hidden layer 256 wide, 8 <= L <= 16 and no skip layers");
+    }
     if (dtype == MARF_BF16X3 && n->s2.variant < 0) {
         delete n;
         return fail(MARF_ERR_UNSUPPORTED,
@@ -515,6 +536,7 @@ int marf_net_layer_span(const marf_net* net, int l, long long* off, long long* l
 }
 const char* marf_net_step_kernel(const marf_net* net) {
     if (!net) return "";
+    if (net->s2.variant == 3) return "k_step2h";
     if (net->s2.variant >= 0) return "k_step2";
     return "k_mlp_step";
 }
@@ -543,7 +565,7 @@ int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, vo
     MarfProfScope ps("pack_weights", (hipStream_t)stream);
     // the tile kernels' layouts (Wf / Wt / bias): every path of a split-bf16 net runs k_step2's
     // program instead (marf_forward / marf_backward refuse it), so it packs that one only
-    if (net->dtype != MARF_BF16X3)
+    if (!split_recipe(net->dtype))
         HIPCHK(marf_launch_pack(net->kdt, d_params, (char*)d_packed, a, mx, (hipStream_t)stream), "net_pack");
     if (net->s2.variant >= 0) {
         const Step2NetPlan& q = net->s2;
@@ -554,7 +576,8 @@ int marf_net_pack(const marf_net* net, const float* d_params, void* d_packed, vo
         b.nk0 = q.nk0;
         b.nta = q.nta;
         b.NKH = q.HM / 16;
-        b.split = q.variant == 1;
+        b.split = q.variant == 1 || q.variant == 3;
+        b.fwd_f16 = q.variant == 3;
         b.slot_bytes = q.slot;
         b.n_stages = q.n_stages;
         b.r0 = q.r0;
@@ -676,8 +699,8 @@ size_t marf_workspace_bytes(const marf_net* net, const marf_geometry* geo) {
 int marf_forward(const marf_net* net, const marf_geometry* geo, const marf_c2f* c2f, const void* d_packed,
                  float* d_rgb, void* d_saved, void* stream) {
     if (!net || !d_packed || !d_rgb) return fail(MARF_ERR_INVALID, "forward: NULL argument");
-    if (net->dtype == MARF_BF16X3)  // the generic kernels have no split-bf16 arithmetic
-        return fail(MARF_ERR_UNSUPPORTED, "forward: split-bf16 nets run marf_step_forward / marf_render only");
+    if (split_recipe(net->dtype))  // the generic kernels have no split arithmetic
+        return fail(MARF_ERR_UNSUPPORTED, "forward: split-recipe nets run marf_step_forward / marf_render only");
     FwdArgs a;
     memset(&a, 0, sizeof(a));
     int rc = make_geo(geo, a.geo, MARF_TILE_PAD);
@@ -707,8 +730,8 @@ int marf_backward(const marf_net* net, const marf_geometry* geo, const marf_c2f*
                   void* stream) {
     if (!net || !d_packed || !d_rgb_out || !d_drgb || !d_saved || !d_workspace)
         return fail(MARF_ERR_INVALID, "backward: NULL argument");
-    if (net->dtype == MARF_BF16X3)
-        return fail(MARF_ERR_UNSUPPORTED, "backward: split-bf16 nets run marf_step_backward only");
+    if (split_recipe(net->dtype))
+        return fail(MARF_ERR_UNSUPPORTED, "backward: split-recipe nets run marf_step_backward only");
     hipStream_t s = (hipStream_t)stream;
     BwdArgs a;
     memset(&a, 0, sizeof(a));
@@ -852,7 +875,24 @@ struct Step2BufPlan {
     int nblk;  // per-block partial sets of the step kernel (all pieces' blocks)
     long long S;
     PipePlan pipe;
+    bool fused_res;  // partl / bpartl reserved for the fused weight gradients (step2_backward takes
+                     // that path only then)
 };
+
+// Can the fused weight gradients (marf_launch_wgrad_fused) run this net?  A superset of what
+// marf_wgrad_fused_ok accepts (every hidden layer one 256 x 256 output block, the A/B switch
+// MARF_WGRAD_FUSED not "0", read once per process so the buffer plan at allocation and at the
+// backward agree): only then does plan_step2_bufs reserve every layer's partials at once.
+static bool step2_fused_wgrad_possible(const marf_net* n) {
+    static const bool env_off = [] {
+        const char* e = getenv("MARF_WGRAD_FUSED");
+        return e && e[0] == '0';
+    }();
+    if (env_off) return false;
+    for (int l = 1; l < n->n_layers - 1; ++l)
+        if (n->Mp[l] != 256 || n->Kp[l] != 256) return false;
+    return true;
+}
 
 static int device_cus() {
     static int cus[64] = {0};
@@ -879,7 +919,7 @@ static long long wgrad_chunk(long long S) {
 static bool l0_recompute(const marf_net* n, const GeoDev& g, long long S) {
     const char* e = getenv("MARF_F0_RECOMPUTE");
     if (e && e[0] == '0') return false;
-    if (n->s2.variant != 1 || g.mode != MARF_GEO_GRID) return false;
+    if ((n->s2.variant != 1 && n->s2.variant != 3) || g.mode != MARF_GEO_GRID) return false;
     const long long chunk = wgrad_chunk(S);
     return marf_wgrad_l0_recompute_ok(n->Mp[0], n->Kp[1], n->s2.ldf0, S, (int)chunk, (int)((S + chunk - 1) / chunk),
                                       g.Np_pad);
@@ -901,7 +941,7 @@ static void plan_pipe(const marf_net* n, const GeoDev& g, long long S, int n_til
     memset(&pp, 0, sizeof(pp));
     const Step2NetPlan& q = n->s2;
     const int mode = n->pipe_mode;  // 0 off (default), 1 on at any size, -1 large steps only
-    if (mode == 0 || q.variant < 0 || g.mode != MARF_GEO_GRID) return;
+    if (mode == 0 || q.variant < 0 || q.variant == 3 || g.mode != MARF_GEO_GRID) return;  // (fp16x2: not piecewise)
     const int cus = device_cus();
     int R = n->pipe_wg > 0 ? n->pipe_wg : std::max(1, cus * 7 / 64);  // 28 of 256 CUs
     R = std::max(1, std::min(R, cus / 2));
@@ -974,13 +1014,17 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
     if (const char* e = getenv("MARF_STEP2_GRID")) cap = std::max(1, atoi(e));  // diagnostic override
     p.grid = std::max(1, std::min(p.n_tiles, cap));
     memset(&p.pipe, 0, sizeof(p.pipe));
+    p.fused_res = false;
     if (!render) plan_pipe(n, g, p.S, p.n_tiles, p.pipe);
     if (p.pipe.on) p.grid = p.pipe.G;
     p.nblk = p.pipe.on ? p.pipe.P * p.pipe.G : p.grid;
     size_t off = 0;
+    // (fp16x2: feat_l carries the 32 NW sink rows too -- a group's missing second set runs its
+    //  forward and stores there)
+    const long long Sfeat = p.S + (q.variant == 3 ? q.TPX : 0);
     for (int l = 0; l < nl - 1; ++l) {
         p.feat[l] = off;
-        off += rup(Ssave * p.S * (l == 0 ? q.ldf0 : n->Kp[l]) * 2, 256);
+        off += rup(Ssave * Sfeat * (l == 0 ? q.ldf0 : n->Kp[l]) * 2, 256);
     }
     p.dz[0] = 0;
     // dz_l and the dH partials carry 32 NW sink rows past S: the dgrad pass of a pixel set that has
@@ -1029,10 +1073,15 @@ static void plan_step2_bufs(const marf_net* n, const GeoDev& g, Step2BufPlan& p,
         off += rup(Ssave * std::max(n_chunks * mxo, 256LL * (3 * q.Kl + 3)) * 4, 256);
         p.bpart = off;
         off += rup(Ssave * n_chunks * mxm * 4, 256);
-        // the fused weight gradients keep every layer's partials at once (layer 0: part)
+        // the fused weight gradients keep every layer's partials at once (layer 0: part); the
+        // per-layer path reuses part / bpart for every layer, so nothing more is reserved for it
+        p.fused_res = !render && step2_fused_wgrad_possible(n);
         p.partl[0] = p.part;
         p.bpartl[0] = p.bpart;
         for (int l = 1; l < nl - 1; ++l) {
+            p.partl[l] = p.part;
+            p.bpartl[l] = p.bpart;
+            if (!p.fused_res) continue;
             p.partl[l] = off;
             off += rup(Ssave * n_chunks * n->Mp[l] * n->Kp[l] * 4, 256);
             p.bpartl[l] = off;
@@ -1076,7 +1125,7 @@ static hipError_t launch_s2(const marf_net* n, const Step2Args& a, int grid, hip
     const Step2NetPlan& q = n->s2;
     // the compile-time layer-0 instantiations: split recipe, every hidden layer 256 wide, the
     // layer-0 row tiles per stage the kernel derives from nk0, a 256-wide last-layer input
-    bool full = q.variant == 1 && q.nk0 >= 1 && q.r0 == std::max(1, std::min(8, 16 / q.nk0)) && q.Kl == 256;
+    bool full = (q.variant == 1 || q.variant == 3) && q.nk0 >= 1 && q.r0 == std::max(1, std::min(8, 16 / q.nk0)) && q.Kl == 256;
     for (int l = 0; l < n->n_layers - 1; ++l) full = full && n->Mp[l] == 256;
     if (const char* e = getenv("MARF_STEP2_GENERIC")) full = full && e[0] != '1';  // (A/B: the generic kernel)
     return marf_launch_step2(a, q.variant, grid, s, full ? q.nk0 : 0, q.dz);
@@ -1141,7 +1190,8 @@ static int step2_forward(const marf_net* net, const marf_geometry* geo, const ma
     const int TPX = q.TPX;
     int off = q.nslot * q.slot;
     a.lds_pro = off;
-    off += 2 * (4 * TPX + 64) * 4;
+    // input buffers: two of (targets + mask + H) per tile; fp16x2: four H rows + two target sets
+    off += q.variant == 3 ? 1024 + 2 * 4 * TPX * 4 : 2 * (4 * TPX + 64) * 4;
     a.lds_bias = off;
     off += (int)rup(q.nbias * 4, 16);
     a.lds_c2f = off;
@@ -1224,7 +1274,7 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
     // The fused weight gradients (marf_launch_wgrad_fused): the hidden layers in one launch, layer 0
     // beside it on the side stream, every reduction in one launch -- the same partials and sums as
     // the per-layer launches below (bit-identical).  The layer events follow it, in the per-layer order.
-    if (d_dparams && !p.pipe.on) {
+    if (d_dparams && !p.pipe.on && p.fused_res) {
         const long long chunk = wgrad_chunk(p.S);
         const int n_chunks = (int)((p.S + chunk - 1) / chunk);
         const int* kmap = (const int*)(sv + p.kmap);
@@ -1559,18 +1609,45 @@ int marf_erode_rect(const float* d_img, int n_img, int H, int W, int kh, int kw,
     return MARF_OK;
 }
 
+}  // extern "C"
+
+// torch.optim.Adam's per-step scalars: bias corrections in python float64, step_size = lr / bc1,
+// bc2 ** 0.5, handed to the kernel as float
+static void adam_scalars(double lr, double beta1, double beta2, long long step, float& step_size, float& bc2_sqrt) {
+    const double bc1 = 1.0 - std::pow(beta1, (double)step);
+    const double bc2 = 1.0 - std::pow(beta2, (double)step);
+    step_size = (float)(lr / bc1);
+    bc2_sqrt = (float)std::sqrt(bc2);
+}
+
+extern "C" {
+
 int marf_adam_step(float* d_p, const float* d_g, float* d_m, float* d_v, long long n, double lr, double beta1,
                    double beta2, double eps, long long step, const float* d_grad_scale, void* stream) {
     if (n < 0 || step < 1 || (n > 0 && (!d_p || !d_g || !d_m || !d_v))) return fail(MARF_ERR_INVALID, "adam: bad args");
-    // torch.optim.Adam: bias corrections in python float64, step_size = lr / bc1, bc2 ** 0.5
-    double bc1 = 1.0 - std::pow(beta1, (double)step);
-    double bc2 = 1.0 - std::pow(beta2, (double)step);
-    double step_size = lr / bc1;
-    double bc2_sqrt = std::sqrt(bc2);
+    float step_size, bc2_sqrt;
+    adam_scalars(lr, beta1, beta2, step, step_size, bc2_sqrt);
     MarfProfScope ps("adam", (hipStream_t)stream);
     HIPCHK(marf_launch_adam(d_p, d_g, d_m, d_v, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
-                            (float)step_size, (float)bc2_sqrt, (float)eps, d_grad_scale, (hipStream_t)stream),
+                            step_size, bc2_sqrt, (float)eps, d_grad_scale, (hipStream_t)stream),
            "adam");
+    return MARF_OK;
+}
+
+int marf_adam_schedule(double lr, double beta1, double beta2, long long first_step, long long count, float* h_out) {
+    if (first_step < 1 || count < 0 || (count > 0 && !h_out)) return fail(MARF_ERR_INVALID, "adam_schedule: bad args");
+    for (long long i = 0; i < count; ++i) adam_scalars(lr, beta1, beta2, first_step + i, h_out[2 * i], h_out[2 * i + 1]);
+    return MARF_OK;
+}
+
+int marf_adam_step_sched(float* d_p, const float* d_g, float* d_m, float* d_v, long long n, double beta1, double beta2,
+                         double eps, const float* d_sched, const int* d_index, const float* d_grad_scale, void* stream) {
+    if (n < 0 || (n > 0 && (!d_p || !d_g || !d_m || !d_v || !d_sched || !d_index)))
+        return fail(MARF_ERR_INVALID, "adam_step_sched: bad args");
+    MarfProfScope ps("adam", (hipStream_t)stream);
+    HIPCHK(marf_launch_adam_sched(d_p, d_g, d_m, d_v, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
+                                  d_sched, d_index, (float)eps, d_grad_scale, (hipStream_t)stream),
+           "adam_step_sched");
     return MARF_OK;
 }
 

@@ -116,6 +116,7 @@ struct Step2Args {
 
 struct Pack2Args {
     int nl, L, nk0, nta, NKH, split, slot_bytes, n_stages;
+    int fwd_f16;                     // forward stages in fp16 hi + lo (the fp16x2 recipe)
     int r0, ns0;                     // layer-0 row tiles per stage, layer-0 stages
     int dims[MARF_MAX_LAYERS + 1];   // true widths
     int nrt[MARF_MAX_LAYERS], nrtb[MARF_MAX_LAYERS];
@@ -202,6 +203,9 @@ hipError_t marf_launch_mse_bwd(const float* pred, const float* gt, const float* 
 hipError_t marf_launch_adam(float* p, const float* g, float* m, float* v, long long n, float w1, float b2,
                             float one_minus_b2, float step_size, float bc2_sqrt, float eps, const float* grad_scale,
                             hipStream_t s);
+hipError_t marf_launch_adam_sched(float* p, const float* g, float* m, float* v, long long n, float w1, float b2,
+                                  float one_minus_b2, const float* sched, const int* index, float eps,
+                                  const float* grad_scale, hipStream_t s);
 hipError_t marf_launch_pack(int dtype, const float* params, char* packed, const marf::PackArgs& a,
                             long long max_elems, hipStream_t s);
 hipError_t marf_launch_pixel_grid(const GeoDev& g, float* xy, int n, hipStream_t s);

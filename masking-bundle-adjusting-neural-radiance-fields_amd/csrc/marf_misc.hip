@@ -96,9 +96,9 @@ __global__ void k_mse_backward(const float* __restrict__ pred, const float* __re
 
 // torch.optim.Adam (foreach form): m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g g;
 // p -= step_size * m / (sqrt(v) / sqrt(bc2) + eps).  grad_scale multiplies g first (1 = none).
-__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                       float* __restrict__ v, long long n, float w1, float b2, float one_minus_b2,
-                       float step_size, float bc2_sqrt, float eps, const float* __restrict__ grad_scale) {
+MARF_DEV void adam_body(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                        float* __restrict__ v, long long n, float w1, float b2, float one_minus_b2, float step_size,
+                        float bc2_sqrt, float eps, const float* __restrict__ grad_scale) {
     const float gsc = grad_scale ? grad_scale[0] : 1.0f;
     for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
         float gi = g[i] * gsc;
@@ -111,6 +111,20 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
         float denom = sqrtf(vi) / bc2_sqrt + eps;
         p[i] = p[i] - step_size * (mi / denom);
     }
+}
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, long long n, float w1, float b2, float one_minus_b2,
+                       float step_size, float bc2_sqrt, float eps, const float* __restrict__ grad_scale) {
+    adam_body(p, g, m, v, n, w1, b2, one_minus_b2, step_size, bc2_sqrt, eps, grad_scale);
+}
+// the step's scalars from a device schedule row (sched[2 s], sched[2 s + 1], s = *index): the same
+// update with host-free per-step values, so a captured training iteration can replay it
+__global__ void k_adam_sched(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, long long n, float w1, float b2, float one_minus_b2,
+                             const float* __restrict__ sched, const int* __restrict__ index, float eps,
+                             const float* __restrict__ grad_scale) {
+    const int s = *index;
+    adam_body(p, g, m, v, n, w1, b2, one_minus_b2, sched[2 * s], sched[2 * s + 1], eps, grad_scale);
 }
 
 // ------------------------------------------------------------------ packing
@@ -352,6 +366,15 @@ hipError_t marf_launch_adam(float* p, const float* g, float* m, float* v, long l
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_adam, dim3(grid_for(n)), dim3(256), 0, s, p, g, m, v, n, w1, b2, one_minus_b2, step_size,
                        bc2_sqrt, eps, grad_scale);
+    return hipGetLastError();
+}
+
+hipError_t marf_launch_adam_sched(float* p, const float* g, float* m, float* v, long long n, float w1, float b2,
+                                  float one_minus_b2, const float* sched, const int* index, float eps,
+                                  const float* grad_scale, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_adam_sched, dim3(grid_for(n)), dim3(256), 0, s, p, g, m, v, n, w1, b2, one_minus_b2, sched,
+                       index, eps, grad_scale);
     return hipGetLastError();
 }
 

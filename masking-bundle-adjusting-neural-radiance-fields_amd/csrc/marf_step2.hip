@@ -98,8 +98,17 @@ MARF_DEV float s2_hi16(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
 union S2Frag {
     bf16x8 f;
+    f16x8 h;  // (the fp16-forward recipe's operands)
     uint4 u;
+    uint32_t w[4];
 };
+
+// two floats -> packed fp16 pair (v_cvt_pk_f16_f32, RNE)
+MARF_DEV uint32_t s2_pkh(float a, float b) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(((f32x2){a, b}), f16x2));
+}
 
 // 8 floats -> bf16 hi fragment (+ lo remainder fragment)
 template <bool LO>
@@ -162,13 +171,20 @@ struct S2Cfg {
 // W_hi^T dz_hi + W_lo^T dz_hi + W_hi^T dz_lo (the forward's three terms), one pixel set per dgrad
 // pass; dz_1 (the layer-0 adjoint's operand) and the saved dz stay bf16 hi.  DESIGN.md §4: the
 // recipe whose emulation reaches fp32's basin rate.
-template <int HM, bool SPLIT, int NW, int MAXR, int NK0F, int NTAF, bool DZ>
+// HF (the fp16x2 recipe, MARF_FP16X2): the forward in fp16 -- weights fp16 hi + lo, activations
+// single fp16, W_hi a + W_lo a (2 MFMAs per MAC instead of 3) -- and, since one 32-pixel set's
+// operands then take half the registers, the forward of a group's TWO tiles in one pass over the
+// forward stages (every weight fragment read from LDS once for both sets, every stage DMA'd once per
+// pair of tiles, as the dgrad already is).  The dgrad, the saved tensors (bf16) and the weight
+// gradients are the split recipe's.  Compile-time layer-0 instantiations only (full-width nets).
+template <int HM, bool SPLIT, int NW, int MAXR, int NK0F, int NTAF, bool DZ, bool HF = false>
 __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Args& a) {
     typedef S2Cfg<HM, SPLIT, NW, MAXR, DZ> C;
     constexpr bool SDZ = SPLIT && DZ;
     constexpr int NKH = C::NKH, NRT = C::NRT, NS = C::NS;
     constexpr bool FIX = NK0F > 0;
     static_assert(NK0F <= C::NK0, "layer-0 k-steps");
+    static_assert(!HF || (SPLIT && !DZ && NK0F > 0 && NS == 2), "fp16x2: split dgrad, two sets, compile-time layer 0");
     constexpr int R0Q = NKH / (FIX ? NK0F : NKH);  // layer-0 row tiles per stage (the host's r0)
     constexpr int R0F = R0Q < 1 ? 1 : (R0Q > NRT ? NRT : R0Q);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -218,7 +234,9 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
     // Stage order of a group of NS tiles: the forward stages of each tile, then ONE pass of the
     // dgrad stages for all of them (render: forward stages only)
     const int nF = a.n_fwd, nB = a.n_stages - a.n_fwd;
-    const int total = (my_tiles / NS) * (NS * nF + nB) + (my_tiles % NS ? (my_tiles % NS) * nF + nB : 0);
+    // (HF: one pass of the forward stages per group as well)
+    const int total = HF ? ((my_tiles + NS - 1) / NS) * (nF + nB)
+                         : (my_tiles / NS) * (NS * nF + nB) + (my_tiles % NS ? (my_tiles % NS) * nF + nB : 0);
 
     // ---- per-tile input DMA: target r, g, b, mask (TPX floats each) and H (9 floats) of a tile
     auto pro_buf = [&](int pb) -> float* { return reinterpret_cast<float*>(smem + a.lds_pro + pb * (4 * C::TPX + 64) * 4); };
@@ -239,6 +257,44 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                  __builtin_amdgcn_readfirstlane(base + 4 * C::TPX * 4));
     };
 
+    // ---- HF: the per-group inputs.  The H rows of a group's two tiles go to H buffer (group parity,
+    // set) at the previous group's first layer-0 stage; the targets / masks of its two tiles to target
+    // buffer (set) at the previous group's first dgrad stage, after its last layer read them.  A
+    // group's missing second tile (odd tile count) repeats the first one's inputs.
+    auto hf_tile = [&](int ti) -> int { return tbase + min(ti, my_tiles - 1) * (int)gridDim.x; };
+    auto proH = [&](int par, int set) -> const float* {
+        return reinterpret_cast<const float*>(smem + a.lds_pro + (par * 2 + set) * 256);
+    };
+    auto proT = [&](int set) -> const float* {
+        return reinterpret_cast<const float*>(smem + a.lds_pro + 1024 + set * C::TPX * 16);
+    };
+    auto issue_h = [&](int ti, int par) {  // 2 vector-memory operations per wave
+#pragma unroll
+        for (int set = 0; set < 2; ++set) {
+            const int b = hf_tile(ti + set) / tpp;
+            s2_glds4(a.geo.Hm ? a.geo.Hm + 9 * (size_t)b + (lane < 9 ? lane : 0) : a.pro_fallback,
+                     __builtin_amdgcn_readfirstlane(lds0 + a.lds_pro + (par * 2 + set) * 256));
+        }
+    };
+    auto issue_tgt = [&](int ti) {  // 4 vector-memory operations per wave
+#pragma unroll
+        for (int set = 0; set < 2; ++set) {
+            const int tile = hf_tile(ti + set);
+            const int b = tile / tpp, q0 = (tile - b * tpp) * C::TPX;
+            const unsigned base = lds0 + a.lds_pro + 1024 + set * C::TPX * 16;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int f = ((wave * 2 + i) * 64) + lane;  // float index in [0, 4 TPX)
+                const int ch = f / C::TPX, q = f - ch * C::TPX;
+                const int p = min(q0 + q, Np - 1);
+                const float* src = !a.gt ? a.pro_fallback
+                                   : ch < 3 ? a.gt + ((size_t)b * 3 + ch) * Np + p
+                                            : (a.mask ? a.mask + (size_t)b * Np + p : a.gt + (size_t)b * 3 * Np + p);
+                s2_glds4(src, __builtin_amdgcn_readfirstlane(base + (wave * 2 + i) * 256));
+            }
+        }
+    };
+
     // ---- the weight ring
     int c_stage = 0;         // global stage counter of this block
     int dma_stage = 0;       // next stage whose DMA is to be issued
@@ -246,7 +302,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
     int dg_i = 0, dg_n = 0, dg_ns = 0, dg_t = 0;
     auto grp_init = [&](int t) {
         dg_t = t;
-        dg_ns = min(NS, my_tiles - t);
+        dg_ns = HF ? 1 : min(NS, my_tiles - t);  // (HF: the forward stages once per group)
         dg_n = dg_ns * nF + nB;
         dg_i = 0;
     };
@@ -327,7 +383,12 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
     };
 
     if (my_tiles > 0) {
-        issue_pro(tbase, 0);
+        if constexpr (HF) {
+            issue_h(0, 0);
+            issue_tgt(0);
+        } else {
+            issue_pro(tbase, 0);
+        }
         dma_arm();
         dma_burst();
         dma_arm();
@@ -675,6 +736,163 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
         }
         store_rt(row0, rtc, O[2 * rt], O[2 * rt + 1]);
     };
+    // ---- the fp16x2 forward (HF): helpers
+    // one 32-row output tile of BOTH pixel sets: c_s += A_hi . B_s + A_lo . B_s over NK k-steps (fp16
+    // MFMAs), each A fragment read from LDS once for the two sets.  Per k-step the order is (set 0,
+    // hi), (set 1, hi), (set 0, lo), (set 1, lo): each set's chain is hi, lo per k-step, as one set
+    // alone would run it.  hook(ks, p) runs in the gap after MFMA p (0..3) of k-step ks.
+    auto gemm2 = [&](f32x16& c0, f32x16& c1, const char* slot, const S2Frag* B0, const S2Frag* B1, auto nk_tag,
+                     auto&& hook, auto pieces_tag) {
+        constexpr int NK = decltype(nk_tag)::value;
+        typedef std::integral_constant<int, 0> P0;
+        typedef std::integral_constant<int, 1> P1;
+        typedef std::integral_constant<int, 2> P2;
+        typedef std::integral_constant<int, 3> P3;
+        const f16x8* ah = reinterpret_cast<const f16x8*>(slot + lane * 16);
+        const f16x8* al = reinterpret_cast<const f16x8*>(slot + C::LO + lane * 16);
+        constexpr int P = NK < 4 ? NK : 4;
+        f16x8 A0[4], A1[4];
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            A0[u] = ah[u * 64];
+            A1[u] = al[u * 64];
+        }
+        s2_sfor<NK>([&](auto ksc) {
+            constexpr int ks = decltype(ksc)::value;
+            constexpr int u = ks & 3;
+            constexpr bool refill = ks + P < NK;
+            __builtin_amdgcn_sched_barrier(0);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0[u], B0[ks].h, c0, 0, 0, 0);
+            hook(ksc, P0());
+            __builtin_amdgcn_sched_barrier(0);
+            c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0[u], B1[ks].h, c1, 0, 0, 0);
+            hook(ksc, P1());
+            if constexpr (refill) A0[u] = ah[(ks + P) * 64];
+            __builtin_amdgcn_sched_barrier(0);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1[u], B0[ks].h, c0, 0, 0, 0);
+            hook(ksc, P2());
+            __builtin_amdgcn_sched_barrier(0);
+            c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1[u], B1[ks].h, c1, 0, 0, 0);
+            hook(ksc, P3());
+            if constexpr (refill) A1[u] = al[(ks + P) * 64];
+            piece_at(ksc, nk_tag, pieces_tag);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    };
+    // epilogue of a 32-row accumulator tile of set s, per pair q of registers (2q, 2q + 1): ReLU of
+    // both (integer max with 0, as frelu), the fp16 operand pair into the next layer's fragment
+    // (k-step 2 rt + q / 4, word q mod 4), the bf16 pair for the saved tensor, its ReLU mask bits
+    // (from the bf16 pair, mask_pair's layout: the dgrad reads them as in the split recipe)
+    struct Ep2 {
+        float x[2][2];
+        uint32_t bw[8];
+        uint32_t bits, mpend;
+    };
+    Ep2 e2[2];
+    auto mask_pair_to = [&](uint32_t& bits, uint32_t w) {
+        uint32_t t;
+        asm volatile(
+            "v_pk_min_u16 %1, %2, %3\n\t"
+            "v_lshl_or_b32 %0, %0, 1, %1"
+            : "+v"(bits), "=&v"(t)
+            : "v"(w), "s"(k_pair1));
+    };
+    // pair operation op (0: ReLU of element 2q, 1: of 2q + 1, 2: the two packs, 3: the mask bits) of
+    // flattened pair PI = 8 s + q, held in temporary slot j
+    auto hop = [&](const f32x16& p0s, const f32x16& p1s, S2Frag* O0, S2Frag* O1, auto rtc, auto pic, auto jc, auto opc) {
+        constexpr int rt = decltype(rtc)::value, PI = decltype(pic)::value, j = decltype(jc)::value;
+        constexpr int op = decltype(opc)::value;
+        if constexpr (PI < 16) {
+            constexpr int sset = PI >> 3, q = PI & 7;
+            const f32x16& pa = sset ? p1s : p0s;
+            Ep2& es = e2[sset];
+            if constexpr (op < 2) {
+                float x;
+                asm volatile("v_max_i32_e32 %0, 0, %1" : "=&v"(x) : "v"(pa[2 * q + op]));
+                es.x[j][op] = x;
+            } else if constexpr (op == 2) {
+                uint32_t w, wb;
+                asm volatile(
+                    "v_cvt_pk_f16_f32 %0, %2, %3\n\t"
+                    "v_cvt_pk_bf16_f32 %1, %2, %3"
+                    : "=&v"(w), "=&v"(wb)
+                    : "v"(es.x[j][0]), "v"(es.x[j][1]));
+                (sset ? O1 : O0)[2 * rt + (q >> 2)].w[q & 3] = w;
+                es.bw[q] = wb;
+            } else {
+                mask_pair_to(es.bits, es.bw[q]);
+            }
+        }
+    };
+    typedef std::integral_constant<int, 0> I0;
+    typedef std::integral_constant<int, 1> I1;
+    typedef std::integral_constant<int, 2> I2;
+    typedef std::integral_constant<int, 3> I3;
+    // the epilogue of row tile rt (accumulators p0s, p1s) in the gaps of the next GEMM: PPK pairs per
+    // k-step, pairs in order (set 0's eight, then set 1's)
+    auto hook2 = [&](const f32x16& p0s, const f32x16& p1s, S2Frag* O0, S2Frag* O1, auto rtc, auto ksc, auto pc,
+                     auto ppkc) {
+        constexpr int ks = decltype(ksc)::value, p = decltype(pc)::value, PPK = decltype(ppkc)::value;
+        typedef std::integral_constant<int, PPK * ks> Pa;
+        typedef std::integral_constant<int, PPK * ks + 1> Pb;
+        if constexpr (PPK == 1) {
+            hop(p0s, p1s, O0, O1, rtc, Pa(), I0(), pc);
+        } else {
+            static_assert(PPK == 2, "pairs per k-step");
+            if constexpr (p == 0) {
+                hop(p0s, p1s, O0, O1, rtc, Pa(), I0(), I0());
+                hop(p0s, p1s, O0, O1, rtc, Pa(), I0(), I1());
+            } else if constexpr (p == 1) {
+                hop(p0s, p1s, O0, O1, rtc, Pa(), I0(), I2());
+                hop(p0s, p1s, O0, O1, rtc, Pb(), I1(), I0());
+            } else if constexpr (p == 2) {
+                hop(p0s, p1s, O0, O1, rtc, Pb(), I1(), I1());
+                hop(p0s, p1s, O0, O1, rtc, Pa(), I0(), I3());
+            } else {
+                hop(p0s, p1s, O0, O1, rtc, Pb(), I1(), I2());
+                hop(p0s, p1s, O0, O1, rtc, Pb(), I1(), I3());
+            }
+        }
+    };
+    // pairs PI0 .. 15 after the GEMM (no gaps left): plain C++, so the compiler interleaves the
+    // pairs' chains; the mask bits in pair order
+    auto free_pairs = [&](const f32x16& p0s, const f32x16& p1s, S2Frag* O0, S2Frag* O1, auto rtc, auto pi0c) {
+        constexpr int rt = decltype(rtc)::value, PI0 = decltype(pi0c)::value;
+        if constexpr (PI0 < 16) {
+            s2_sfor<16 - PI0>([&](auto jc) {
+                constexpr int PI = PI0 + decltype(jc)::value, sset = PI >> 3, q = PI & 7;
+                const f32x16& pa = sset ? p1s : p0s;
+                const float x0 = __int_as_float(max(__float_as_int(pa[2 * q]), 0));
+                const float x1 = __int_as_float(max(__float_as_int(pa[2 * q + 1]), 0));
+                (sset ? O1 : O0)[2 * rt + (q >> 2)].w[q & 3] = s2_pkh(x0, x1);
+                e2[sset].bw[q] = s2_pk(x0, x1);
+            });
+            s2_sfor<16 - PI0>([&](auto jc) {
+                constexpr int PI = PI0 + decltype(jc)::value;
+                mask_pair_to(e2[PI >> 3].bits, e2[PI >> 3].bw[PI & 7]);
+            });
+        }
+    };
+    // finish of row tile rt of set s: the mask word (two row tiles per word) and the bf16 stores
+    auto ffinish2 = [&](int l, auto rtc, auto sc, bool save, u16* srow, bool last) {
+        constexpr int rt = decltype(rtc)::value, sset = decltype(sc)::value;
+        Ep2& es = e2[sset];
+        uint32_t* mks = mkl + sset * C::MSET;
+        if constexpr ((rt & 1) == 0) {
+            es.mpend = es.bits << 8;
+            if (last) mks[(l * C::NMW + (rt >> 1)) * 64 + lane] = es.mpend;
+        } else {
+            mks[(l * C::NMW + (rt >> 1)) * 64 + lane] = es.mpend | es.bits;
+        }
+        if (save) {
+            S2Frag f0, f1;
+            f0.u = make_uint4(es.bw[0], es.bw[1], es.bw[2], es.bw[3]);
+            f1.u = make_uint4(es.bw[4], es.bw[5], es.bw[6], es.bw[7]);
+            store_rt(srow, rtc, f0, f1);
+        }
+    };
+    f32x16 hacc[4];  // HF: current (0, 1) and previous (2, 3) row tile of sets 0, 1 (alternating)
+
     const float pi_f = 3.14159265358979323846f;
 
     // what the dgrad pass keeps of each pixel set's forward: the g operand, the warp's homogeneous
@@ -689,6 +907,244 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
     S2T_BEGIN(7);
     for (int it = 0; it < my_tiles; it += NS) {
         const int nset = min(NS, my_tiles - it);
+        if constexpr (HF) {
+            // ---- the fp16x2 forward of the group's two pixel sets (set 1 of a last, single tile
+            //      repeats set 0's inputs; its stores go to the sink rows, its loss terms are zero)
+            const int gp = (it / NS) & 1;
+            int tl[2];
+            long long sl[2];  // the set's first pixel slot of the wave (a missing set: the sink rows)
+            bool real[2];
+            float Xs[2][3];
+            S2Frag F0[2][NK0F > 0 ? NK0F : 1];
+            s2_sfor<2>([&](auto sc) {
+                constexpr int sset = decltype(sc)::value;
+                real[sset] = it + sset < my_tiles;
+                const int tile = hf_tile(it + sset);
+                tl[sset] = tile;
+                const int b = tile / tpp;
+                const int p0 = (tile - b * tpp) * C::TPX + 32 * wave;
+                sl[sset] = real[sset] ? (long long)b * a.geo.Np_pad + p0 : a.S + 32 * wave;
+                const float* hm = proH(gp, sset);
+                float Hm[9];
+#pragma unroll
+                for (int e = 0; e < 9; ++e) Hm[e] = hm[e];
+                const int p = p0 + pxl;
+                float x, y, u, v, X[3];
+                if (a.geo.mode == 1) {  // explicit coordinates (render only)
+                    const int pc = min(p, Np - 1);
+                    u = x = a.geo.coords[2 * (size_t)pc];
+                    v = y = a.geo.coords[2 * (size_t)pc + 1];
+                    X[0] = u;
+                    X[1] = v;
+                    X[2] = 1.0f;
+                } else {
+                    const int r = p / a.geo.w, cc = p - r * a.geo.w;
+                    x = grid_coord(a.geo.x0 + cc, a.geo.W, a.geo.norm_w);
+                    y = grid_coord(a.geo.y0 + r, a.geo.H, a.geo.norm_h);
+                    warp_point(Hm, x, y, u, v, X, a.geo.bmm_small);
+                }
+                Xs[sset][0] = X[0];
+                Xs[sset][1] = X[1];
+                Xs[sset][2] = X[2];
+                const float cd = h ? v : u;
+                // posenc + c2f: band groups of 4 (sin, cos) and the raw coordinate, as fp16 operands;
+                // feat_0 (bf16) only when the layer-0 weight gradient does not recompute it
+                const bool st0 = !a.fwd_only && !a.feat0_recompute;
+                u16* row0 = st0 ? ly_ptr(0, 0) + (sl[sset] >> 5) * ly_int(0, 3) * 32 + pxl * 16 + 8 * h : nullptr;
+                s2_sfor<NK0F>([&](auto gc) {
+                    constexpr int g = decltype(gc)::value;
+                    float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                    if constexpr (g < NK0F - 1) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int k = 4 * g + j;
+                            float sn = 0.f, co = 0.f;
+                            if (k < L) {
+                                band_sincos<true>(cd, k, sn, co);
+                                if (a.c2f_on) {
+                                    const float w = c2f_l[k];
+                                    sn = sn * w;
+                                    co = co * w;
+                                }
+                            }
+                            f[j] = sn;
+                            f[4 + j] = co;
+                        }
+                    } else {
+                        f[0] = cd;
+                    }
+                    F0[sset][g].u = make_uint4(s2_pkh(f[0], f[1]), s2_pkh(f[2], f[3]), s2_pkh(f[4], f[5]), s2_pkh(f[6], f[7]));
+                    if (st0) s2_st16(row0 + 512 * g, make_uint4(s2_pk(f[0], f[1]), s2_pk(f[2], f[3]), s2_pk(f[4], f[5]), s2_pk(f[6], f[7])));
+                });
+                if (st0) {
+                    st_cur += NK0F;
+                    if (16 * NK0F < ly_int(0, 3)) {
+                        s2_st16(row0 + 512 * NK0F, make_uint4(0, 0, 0, 0));
+                        st_cur += 1;
+                    }
+                }
+            });
+            // ---- forward, layer 0 then the hidden layers: one stage per 32-row output tile (layer
+            //      0: r0 row tiles per stage); the epilogue of row tile rt-1 of both sets runs in the
+            //      MFMA gaps of row tile rt, the last row tile's right after its own MFMAs
+            auto fwd2_layer = [&](int l, const S2Frag* B0, const S2Frag* B1, auto nk_tag, auto ppk_tag) {
+                constexpr int NK = decltype(nk_tag)::value, PPK = decltype(ppk_tag)::value;
+                typedef std::integral_constant<bool, NK == NKH> PcL;  // hidden: pieces in the GEMM
+                const bool save = l + 1 < nl - 1 && !a.fwd_only;
+                u16* srow[2];
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    srow[q] = save ? ly_ptr(l + 1, 0) + (sl[q] >> 5) * ly_int(l + 1, 3) * 32 + pxl * 16 + 8 * h : nullptr;
+                const int boff = ly_int(l, 2);
+                const char* slotb = nullptr;
+                s2_sfor<NRT>([&](auto rtc) {
+                    constexpr int rt = decltype(rtc)::value;
+                    f32x16& c0 = hacc[(rt & 1) ? 2 : 0];
+                    f32x16& c1 = hacc[(rt & 1) ? 3 : 1];
+                    f32x16& q0 = hacc[(rt & 1) ? 0 : 2];
+                    f32x16& q1 = hacc[(rt & 1) ? 1 : 3];
+                    const int sub = l == 0 ? rt % R0F : 0;
+                    c0 = bias_init(boff, rt);  // (before the stage wait: the reads overlap it)
+                    c1 = c0;
+                    if (sub == 0) slotb = stage_begin(l == 0);  // layer 0: the pieces in a burst
+                    const char* slot = slotb + sub * NK * 1024;
+                    if (l == 0 && rt == 0 && it + NS < my_tiles) {
+                        issue_h(it + NS, gp ^ 1);  // (the buffer's last reader finished before this barrier)
+                        st_cur += 2;
+                    }
+                    if constexpr (rt == 0) {
+                        gemm2(c0, c1, slot, B0, B1, nk_tag, nohook, PcL());
+                    } else {
+                        typedef std::integral_constant<int, rt - 1> RP;
+                        e2[0].bits = 0;
+                        e2[1].bits = 0;
+                        gemm2(c0, c1, slot, B0, B1, nk_tag, [&](auto ksc, auto pc) {
+                            hook2(q0, q1, Oh, Ol, RP(), ksc, pc, ppk_tag);
+                        }, PcL());
+                        free_pairs(q0, q1, Oh, Ol, RP(), std::integral_constant<int, PPK * NK>());
+                        ffinish2(l, RP(), I0(), save, srow[0], false);
+                        ffinish2(l, RP(), I1(), save, srow[1], false);
+                    }
+                    if constexpr (rt == NRT - 1) {
+                        e2[0].bits = 0;
+                        e2[1].bits = 0;
+                        free_pairs(c0, c1, Oh, Ol, rtc, I0());
+                        ffinish2(l, rtc, I0(), save, srow[0], true);
+                        ffinish2(l, rtc, I1(), save, srow[1], true);
+                    }
+                });
+#pragma unroll
+                for (int k = 0; k < NKH; ++k) {
+                    Bh[k] = Oh[k];
+                    Bl[k] = Ol[k];
+                }
+            };
+            fwd2_layer(0, F0[0], F0[1], std::integral_constant<int, NK0F>(), I2());
+            for (int l = 1; l < nl - 1; ++l) fwd2_layer(l, Bh, Bl, NKHt(), I1());
+
+            // ---- last layer of both sets: 3 outputs (rows 0..2 of one tile), sigmoid, masked MSE, d rgb
+            float gS[2][3];
+            {
+                f32x16& c0 = hacc[0];
+                f32x16& c1 = hacc[1];
+                c0 = bias_init(ly_int(nl - 1, 2), 0);
+                c1 = c0;
+                const char* slot = stage_begin(false);
+                gemm2(c0, c1, slot, Bh, Bl, NKHt(), nohook, PcOn());
+                s2_sfor<2>([&](auto sc) {
+                    constexpr int sset = decltype(sc)::value;
+                    const f32x16& acc = sset ? c1 : c0;
+                    const int b = tl[sset] / tpp;
+                    const int p = (tl[sset] - b * tpp) * C::TPX + 32 * wave + pxl;
+                    const bool valid = real[sset] && p < Np;
+                    const float* pt = proT(sset);
+                    float* o = (a.rgb && valid && h == 0) ? a.rgb + ((size_t)b * Np + p) * 3 : dmy;
+                    float yv[3] = {0.f, 0.f, 0.f};
+                    gS[sset][0] = gS[sset][1] = gS[sset][2] = 0.f;
+                    if (h == 0) {
+                        const float m = valid ? (a.mask ? pt[3 * C::TPX + 32 * wave + pxl] : 1.0f) : 0.f;
+                        float sqf = 0.f;
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) {
+                            const float z = acc[c];
+                            const float yy = 1.0f / (1.0f + expf(-z));
+                            yv[c] = yy;
+                            const float t = valid ? pt[c * C::TPX + 32 * wave + pxl] : 0.f;
+                            // model/planar.py:388-390 and its autograd: x = (p - g) m, d = 2 x m
+                            const float xx = (yy - t) * m;
+                            sqf += xx * xx;
+                            const float d = (2.0f * xx) * m;
+                            gS[sset][c] = (d * (1.0f - yy)) * yy;  // sigmoid backward
+                        }
+                        lsq += (double)sqf;
+                        lms += (double)m;
+                        bl0 += gS[sset][0];
+                        bl1 += gS[sset][1];
+                        bl2 += gS[sset][2];
+                    }
+                    s2_st12(o, yv[0], yv[1], yv[2]);
+                    st_cur += 1;
+                });
+            }
+            if (a.fwd_only) continue;  // render: the program holds the forward stages only
+            s2_sfor<2>([&](auto sc) {
+                constexpr int sset = decltype(sc)::value;
+                // g operand of the last-layer dgrad (bf16, as the split recipe): lane half 0,
+                // k = [g hi (3), 0, g lo (3), 0]
+                S2Frag Bg;
+                {
+                    float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                    if (h == 0) {
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) {
+                            f[c] = gS[sset][c];
+                            f[4 + c] = gS[sset][c] - s2_lo16(s2_pk(gS[sset][c], 0.f));
+                        }
+                    }
+                    S2Frag dumm;
+                    s2_split8<false>(f, Bg, dumm);
+                }
+                // last-layer weight gradient of the set's 32 pixels in fp16 (the operand the forward
+                // used): A = (2^10 g)^T as fp16 hi (rows 0-2) + lo (rows 4-6) -- an exact power of two
+                // that keeps |g| <= 0.5 in fp16's normal range -- B = feat^T through the LDS transpose
+                {
+                    constexpr float SC = 1024.f;
+                    if (h == 0) {
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) {
+                            const float gs = gS[sset][c] * SC;
+                            const u16 hi = f2h(gs);
+                            gts[c * 32 + pxl] = hi;
+                            gts[(4 + c) * 32 + pxl] = f2h(gs - h2f(hi));
+                        }
+                    }
+                    const f16x8 ga = *reinterpret_cast<const f16x8*>(gts + (lane & 15) * 32 + 8 * (lane >> 4));
+                    const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+                    const S2Frag* Bf = sset ? Bl : Bh;
+#pragma unroll
+                    for (int ks = 0; ks < NKH; ++ks) {
+                        *reinterpret_cast<uint4*>(trs + (pxl * 2 + h) * 8) = Bf[ks].u;
+                        const u16* b0 = trs + (8 * gq + q) * 16 + (pp & 1) * 8 + 4 * (pp >> 1);
+                        i16x4 vv[2] = {s2_tr16(b0), s2_tr16(b0 + 4 * 16)};
+                        const f32x4 r4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ga, *reinterpret_cast<f16x8*>(vv), (f32x4){}, 0, 0, 0);
+                        float lo[3];
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) lo[c] = __shfl_down(r4[c], 16, 64);
+                        if (lane < 16) {
+#pragma unroll
+                            for (int c = 0; c < 3; ++c) wla[c * HM + 16 * ks + lane] += (r4[c] + lo[c]) * (1.0f / SC);
+                        }
+                    }
+                }
+                SetSt cs;
+                cs.g = Bg;
+                cs.X0 = Xs[sset][0];
+                cs.X1 = Xs[sset][1];
+                cs.X2 = Xs[sset][2];
+                cs.tile = real[sset] ? tl[sset] : -1;
+                ss[sset] = cs;
+            });
+        } else {
         for (int si = 0; si < nset; ++si) {
             S2T_BEGIN(4);
             const int ti = it + si;
@@ -968,6 +1424,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             }
             S2T_END(6);
         }
+        }  // (the split recipe's forward, one tile at a time)
         if (a.fwd_only) continue;
         if (nset < NS) {  // no tile for the last set: its dgrad runs on zeros into the store sink rows
             SetSt cs;
@@ -1015,6 +1472,12 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             S2Frag gB[NS];
             s2_sfor<NS>([&](auto sc) { gB[decltype(sc)::value] = ss[decltype(sc)::value].g; });
             const char* slot = stage_begin(true);  // single-k-step GEMMs: the pieces in a burst
+            if constexpr (HF) {
+                if (it + NS < my_tiles) {  // the next group's targets (this group's last layer read its own)
+                    issue_tgt(it + NS);
+                    st_cur += 4;
+                }
+            }
             s2_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;
                 if (rt < nrt) {
@@ -1306,6 +1769,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2dz(Step2Args a) {
     k_step2_body<HM, SPLIT, NW, MAXR, NK0F, NTAF, true>(a);
 }
 
+// the fp16x2 recipe (MARF_FP16X2): fp16 forward of two pixel sets per stage, the split dgrad
+template <int HM, int NW, int MAXR, int NK0F, int NTAF>
+__global__ __launch_bounds__(NW * 64, NW / 4) void k_step2h(Step2Args a) {
+    k_step2_body<HM, true, NW, MAXR, NK0F, NTAF, false, true>(a);
+}
+
 // permuted k (hidden operand from an accumulator): k-step ks, lane half hh, element j
 MARF_DEV int s2_kperm(int ks, int hh, int j) { return 16 * ks + 8 * (j >> 2) + 4 * hh + (j & 3); }
 
@@ -1415,8 +1884,13 @@ __global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog
         }
         u16 out = 0;
         if (have) {
-            const u16 hi = f2bf(val);
-            out = part == 0 ? hi : (a.split ? f2bf(val - bf2f(hi)) : (u16)0);
+            if (a.fwd_f16 && kind <= 1) {  // the fp16x2 recipe's forward stages: fp16 hi + lo
+                const u16 hi = f2h(val);
+                out = part == 0 ? hi : f2h(val - h2f(hi));
+            } else {
+                const u16 hi = f2bf(val);
+                out = part == 0 ? hi : (a.split ? f2bf(val - bf2f(hi)) : (u16)0);
+            }
         }
         prog[e] = out;
     }
@@ -1426,14 +1900,17 @@ __global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog
 
 using namespace marf;
 
-template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0, int NTAF = 0, bool DZ = false>
+template <int HM, bool SPLIT, int NW, int MAXR, int NK0F = 0, int NTAF = 0, bool DZ = false, bool HF = false>
 static hipError_t launch_step2_t(const Step2Args& a, int grid, hipStream_t s) {
     const void* k;
-    if constexpr (DZ) k = (const void*)k_step2dz<HM, SPLIT, NW, MAXR, NK0F, NTAF>;
+    if constexpr (HF) k = (const void*)k_step2h<HM, NW, MAXR, NK0F, NTAF>;
+    else if constexpr (DZ) k = (const void*)k_step2dz<HM, SPLIT, NW, MAXR, NK0F, NTAF>;
     else k = (const void*)k_step2<HM, SPLIT, NW, MAXR, NK0F, NTAF>;
     hipError_t e = ensure_dynamic_lds(k, (size_t)a.lds_total);
     if (e != hipSuccess) return e;
-    if constexpr (DZ)
+    if constexpr (HF)
+        hipLaunchKernelGGL((k_step2h<HM, NW, MAXR, NK0F, NTAF>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
+    else if constexpr (DZ)
         hipLaunchKernelGGL((k_step2dz<HM, SPLIT, NW, MAXR, NK0F, NTAF>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
     else
         hipLaunchKernelGGL((k_step2<HM, SPLIT, NW, MAXR, NK0F, NTAF>), dim3(grid), dim3(NW * 64), (size_t)a.lds_total, s, a);
@@ -1441,12 +1918,20 @@ static hipError_t launch_step2_t(const Step2Args& a, int grid, hipStream_t s) {
 }
 
 // variant: 0 = plain bf16, 256-wide, 8 waves; 1 = split bf16, 256-wide, 4 waves; 2 = plain bf16,
-// 256-wide, 4 waves (diagnostic: the variant-0 arithmetic at one wave per SIMD)
+// 256-wide, 4 waves (diagnostic: the variant-0 arithmetic at one wave per SIMD); 3 = fp16x2 (the fp16
+// forward of two pixel sets per stage + the split dgrad), 256-wide, 4 waves
 // full_nk0: a full-width net's layer-0 k-step count (its r0 and row-tile counts follow from it; see
 // k_step2's NK0F), or 0 for the generic instantiation; the compile-time instantiations cover
 // (nk0, nta) = (5, 3): L = 16; (5, 2): L = 13..15; (4, 2): L = 9..12; (3, 2): L = 8
 // dz: the split recipe with the dgrad's dz split too (k_step2's DZ; L = 8 and 16 instantiated)
 hipError_t marf_launch_step2(const Step2Args& a, int variant, int grid, hipStream_t s, int full_nk0, bool dz) {
+    if (variant == 3) {  // fp16x2: the compile-time layer-0 instantiations only
+        if (full_nk0 == 5 && a.nta == 3) return launch_step2_t<256, true, 4, 4, 5, 3, false, true>(a, grid, s);
+        if (full_nk0 == 5 && a.nta == 2) return launch_step2_t<256, true, 4, 4, 5, 2, false, true>(a, grid, s);
+        if (full_nk0 == 4 && a.nta == 2) return launch_step2_t<256, true, 4, 4, 4, 2, false, true>(a, grid, s);
+        if (full_nk0 == 3 && a.nta == 2) return launch_step2_t<256, true, 4, 4, 3, 2, false, true>(a, grid, s);
+        return hipErrorInvalidValue;
+    }
     if (variant == 1 && dz) {
         if (full_nk0 == 5 && a.nta == 3) return launch_step2_t<256, true, 4, 4, 5, 3, true>(a, grid, s);
         if (full_nk0 == 3 && a.nta == 2) return launch_step2_t<256, true, 4, 4, 3, 2, true>(a, grid, s);

@@ -8,13 +8,14 @@ if the library is missing or the tensors are not on a ROCm device the calls rais
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MARF_LIB selects a diagnostic build (lib/libmarf_stamps.so, tools/phase_stamps.py)
 LIB_PATH = os.environ.get("MARF_LIB") or os.path.join(_HERE, "lib", "libmarf.so")
 
-MARF_FP32, MARF_BF16, MARF_BF16X3, MARF_FP16 = 0, 1, 2, 3
+MARF_FP32, MARF_BF16, MARF_BF16X3, MARF_FP16, MARF_FP16X2 = 0, 1, 2, 3, 4
 GEO_GRID, GEO_COORDS, GEO_CANVAS = 0, 1, 2
 
 _c_int, _c_ll, _c_dbl, _c_vp, _c_sz = ctypes.c_int, ctypes.c_longlong, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
@@ -82,6 +83,9 @@ _SIGS = {
     "marf_masked_mse_backward": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "marf_adam_step": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_ll, _c_dbl, _c_dbl, _c_dbl, _c_dbl, _c_ll, _c_vp,
                                 _c_vp]),
+    "marf_adam_schedule": (_c_int, [_c_dbl, _c_dbl, _c_dbl, _c_ll, _c_ll, _c_vp]),
+    "marf_adam_step_sched": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_ll, _c_dbl, _c_dbl, _c_dbl, _c_vp, _c_vp, _c_vp,
+                                      _c_vp]),
     "marf_debug_set_stamps": (None, [_c_vp]),
     "marf_profile_enable": (_c_int, [_c_int]),
     "marf_profile_reset": (_c_int, []),
@@ -902,7 +906,8 @@ def adam_step(p, g, m, v, lr, beta1, beta2, eps, step, grad_scale=None):
 class Adam(torch.optim.Optimizer):
     """torch.optim.Adam (model/planar.py:98-99) with the update in one HIP kernel per contiguous
     parameter segment.  Same constructor, param groups, state keys (step, exp_avg, exp_avg_sq).
-    Parameters with grad None are skipped, as in torch."""
+    Parameters with grad None are skipped, as in torch.  step_scheduled() is the same update with the
+    per-step scalars read on the device (a captured training iteration replays it)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False, **kw):
         if weight_decay != 0 or amsgrad:
@@ -910,51 +915,92 @@ class Adam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
         self._flat_state = {}
 
+    def _segments(self, group, advance):
+        """(param, grad, exp_avg, exp_avg_sq, step) per launch of the group's parameters that have a
+        gradient: one per run of consecutive views (the MLP parameters share one flat buffer), state
+        created (zeros) on first use; advance: each parameter's step += 1 first."""
+        ps = [p for p in group["params"] if p.grad is not None]
+        if not ps:
+            return []
+        runs, cur = [], [ps[0]]
+        for p in ps[1:]:
+            if flat_view(cur + [p]) is not None and flat_view([q.grad for q in cur + [p]]) is not None:
+                cur.append(p)
+            else:
+                runs.append(cur)
+                cur = [p]
+        runs.append(cur)
+        out = []
+        for run in runs:
+            for p in run:
+                st = self.state[p]
+                if not st:
+                    st["step"] = 0
+            if advance:
+                for p in run:
+                    self.state[p]["step"] += 1
+            step = self.state[run[0]]["step"]
+            if len(run) > 1 and all(self.state[p]["step"] == step for p in run):
+                pf = flat_view(run)
+                gf = flat_view([p.grad for p in run])
+                key = tuple(id(p) for p in run)
+                if key not in self._flat_state:
+                    m = torch.zeros_like(pf)
+                    v = torch.zeros_like(pf)
+                    self._flat_state[key] = (m, v)
+                    for p, mm, vv in zip(run, _split_grads(m, [q.shape for q in run]),
+                                         _split_grads(v, [q.shape for q in run])):
+                        self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"] = mm, vv
+                m, v = self._flat_state[key]
+                out.append((pf, gf.contiguous(), m, v, step))
+            else:
+                for p in run:
+                    st = self.state[p]
+                    if "exp_avg" not in st:
+                        st["exp_avg"] = torch.zeros_like(p)
+                        st["exp_avg_sq"] = torch.zeros_like(p)
+                    out.append((p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], st["step"]))
+        return out
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         for group in self.param_groups:
-            ps = [p for p in group["params"] if p.grad is not None]
-            if not ps:
-                continue
             b1, b2 = group["betas"]
-            # one launch per run of consecutive views (the MLP parameters share one flat buffer)
-            runs, cur = [], [ps[0]]
-            for p in ps[1:]:
-                if flat_view(cur + [p]) is not None and flat_view([q.grad for q in cur + [p]]) is not None:
-                    cur.append(p)
-                else:
-                    runs.append(cur)
-                    cur = [p]
-            runs.append(cur)
-            for run in runs:
-                for p in run:
-                    st = self.state[p]
-                    if not st:
-                        st["step"] = 0
-                for p in run:
-                    self.state[p]["step"] += 1
-                step = self.state[run[0]]["step"]
-                if len(run) > 1 and all(self.state[p]["step"] == step for p in run):
-                    pf = flat_view(run)
-                    gf = flat_view([p.grad for p in run])
-                    key = tuple(id(p) for p in run)
-                    if key not in self._flat_state:
-                        m = torch.zeros_like(pf)
-                        v = torch.zeros_like(pf)
-                        self._flat_state[key] = (m, v)
-                        for p, mm, vv in zip(run, _split_grads(m, [q.shape for q in run]),
-                                             _split_grads(v, [q.shape for q in run])):
-                            self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"] = mm, vv
-                    m, v = self._flat_state[key]
-                    adam_step(pf, gf.contiguous(), m, v, group["lr"], b1, b2, group["eps"], step)
-                else:
-                    for p in run:
-                        st = self.state[p]
-                        if "exp_avg" not in st:
-                            st["exp_avg"] = torch.zeros_like(p)
-                            st["exp_avg_sq"] = torch.zeros_like(p)
-                        adam_step(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], group["lr"], b1, b2,
-                                  group["eps"], st["step"])
+            for p, g, m, v, step in self._segments(group, advance=True):
+                adam_step(p, g, m, v, group["lr"], b1, b2, group["eps"], step)
         PARAM_GENERATION[0] += 1
         return loss
+
+    def schedule_tables(self, n_steps, device):
+        """Per group: the [n_steps][2] float32 table of (step_size, sqrt(1 - beta2^k)) for steps
+        k = 1 .. n_steps, as marf_adam_step computes them (marf_adam_schedule), on the device."""
+        tabs = []
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            buf = (ctypes.c_float * (2 * n_steps))()
+            _check(lib().marf_adam_schedule(float(group["lr"]), float(b1), float(b2), 1, int(n_steps), buf))
+            tabs.append(torch.from_numpy(np.ctypeslib.as_array(buf).copy()).to(device))
+        return tabs
+
+    @torch.no_grad()
+    def step_scheduled(self, index, tables, expect_step):
+        """The update of every group with its step's scalars read on the device: row index[0] (device
+        int32, = step - 1) of the group's schedule table.  Host state is not advanced (the caller
+        does, per replay: advance_steps); expect_step = the step this launch sequence is recorded for
+        (every segment's state must be one behind it: one shared index)."""
+        for group, tab in zip(self.param_groups, tables):
+            b1, b2 = group["betas"]
+            for p, g, m, v, step in self._segments(group, advance=False):
+                if step + 1 != expect_step:
+                    raise RuntimeError(f"Adam.step_scheduled: parameter at step {step}, expected {expect_step - 1}")
+                _check(lib().marf_adam_step_sched(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), float(b1), float(b2),
+                                                  float(group["eps"]), _ptr(tab), _ptr(index), None, _stream(p)))
+
+    def advance_steps(self):
+        """Host bookkeeping of one replayed step_scheduled: every parameter with a gradient steps."""
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is not None:
+                    self.state[p]["step"] += 1
+        PARAM_GENERATION[0] += 1

@@ -69,7 +69,9 @@ def _precision(opt):
         return marf_hip.MARF_BF16X3
     if p in ("fp16", "float16", "half"):
         return marf_hip.MARF_FP16
-    raise ValueError(f"precision must be fp32, fp16, bf16 or bf16x3, got {p}")
+    if p in ("fp16x2", "split-fp16"):
+        return marf_hip.MARF_FP16X2
+    raise ValueError(f"precision must be fp32, fp16, bf16, bf16x3 or fp16x2, got {p}")
 
 
 def _dist():
@@ -214,24 +216,40 @@ class Model(torch.nn.Module):
         return loss
 
     def graph_capable(self):
-        """A step can be captured when it has no host-dependent value per step: one process, the
-        fused step, no edge term (its alpha = it / max_iter is a host value)."""
+        """A whole iteration can be captured when it has no host-dependent value per step: one
+        process, the fused step, no edge term (its alpha = it / max_iter is a host value), no
+        learning-rate scheduler, the library's Adam (its per-step scalars come from a device table)."""
         return (self.world == 1 and not self.opt.use_edges and self.opt.get("fused_step", True)
-                and str(self.opt.device).startswith("cuda"))
+                and str(self.opt.device).startswith("cuda") and not self.sched
+                and isinstance(self.optim, marf_hip.Adam))
+
+    def _capture_ident(self, var):
+        return (tuple(int(i) for i in var.idx.tolist()) if torch.is_tensor(var.idx) else tuple(var.idx),
+                var.images.rgb.data_ptr(), var.images.masks.data_ptr() if torch.is_tensor(var.images.get("masks")) else 0,
+                self.graph.neural_image.mlp[0].weight.data_ptr(), self.graph.warp_param.weight.data_ptr())
 
     def captured_step(self, var):
-        """Graph.forward + compute_loss + the weighted loss sum + backward of one training step as a
-        replayed HIP graph (torch.cuda.CUDAGraph).  The first call runs two eager warm-up passes (every
-        buffer and kernel attribute set up) and records the step once; every call replays the
-        recorded launches -- the same kernels on the same buffers with the same arguments, so the
-        same bits as the eager step (test_captured_step_matches_eager) without the per-launch host
-        work.  The weight repack is always recorded (the optimizer updates the weights between
-        replays), the optimizer step, progress update and fix_first stay eager (host values).
-        Returns (var, loss) with the graph's static tensors."""
-        if self._step_graph is None:
+        """One whole training iteration (model/planar.py:187-209 and the loop's fix_first, :154-158)
+        as a replayed HIP graph (torch.cuda.CUDAGraph): Graph.forward + compute_loss + the weighted
+        loss sum + backward + Adam + the progress update + fix_first.  Adam's per-step scalars
+        (bias corrections) come from a device table indexed by a device step counter
+        (marf_adam_step_sched), the progress from a device table of it / max_iter (both computed on
+        the host exactly as the eager step computes them), so every replay is the eager iteration's
+        launches on the same buffers: the same bits (test_captured_step_matches_eager).
+        The first call runs two eager warm-up passes (every buffer and kernel attribute set up),
+        creates the optimizer state and records once; every call replays.  Host bookkeeping per
+        replay: Graph.it, each parameter's Adam step.  The graph is bound to the batch it was
+        recorded with: another var raises.  Returns (var, loss) with the graph's static tensors."""
+        ident = self._capture_ident(var)
+        cap = self._step_graph
+        if cap is not None and max(self.it, cap["adam_step"]) + 1 >= cap["limit"]:
+            cap = self._step_graph = None  # past the recorded tables: record again with longer ones
+        if cap is None:
             if not self.graph_capable():
-                raise RuntimeError("captured_step: needs one process, the fused step and use_edges off")
+                raise RuntimeError("captured_step: needs one process, the fused step, use_edges off, no scheduler "
+                                   "and the library's Adam")
             dev = torch.device(self.opt.device)
+            it0 = self.graph.it
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
@@ -239,24 +257,51 @@ class Model(torch.nn.Module):
                     self.optim.zero_grad(set_to_none=True)
                     v = self.graph.forward(var, mode="train")
                     self._loss_sum(self.graph.compute_loss(v, mode="train")).all.backward()
+                # the optimizer state (zeros) exists before the recording
+                for group in self.optim.param_groups:
+                    self.optim._segments(group, advance=False)
             torch.cuda.current_stream(dev).wait_stream(side)
             self._drop_autograd(var)  # (no warm-up graph, whose gradient nodes live on `side`, stays alive)
             self.graph.neural_image.engine(dev)._packed_version = None  # the repack must be recorded
+            steps = {st["step"] for st in self.optim.state.values() if "step" in st}
+            if len(steps) > 1:
+                raise RuntimeError(f"captured_step: parameters at different Adam steps {sorted(steps)}")
+            adam_step = steps.pop() if steps else 0
+            limit = max(int(self.opt.max_iter), self.it, adam_step) + 1024
+            tabs = self.optim.schedule_tables(limit, dev)
+            # it / max_iter in python float64, then float32: progress.data.fill_ of the eager step
+            ptab = torch.tensor([k / self.opt.max_iter for k in range(limit + 1)], dtype=torch.float32, device=dev)
+            c_adam = torch.tensor([adam_step], dtype=torch.int32, device=dev)
+            c_it = torch.tensor([self.it], dtype=torch.int32, device=dev)
+            progress = self.graph.neural_image.progress
+            fix_first = bool(self.opt.warp.fix_first)
             self.optim.zero_grad(set_to_none=True)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 v = self.graph.forward(var, mode="train")
                 loss = self._loss_sum(self.graph.compute_loss(v, mode="train"))
                 loss.all.backward()
-            # the static outputs, detached: the recorded autograd graph is not needed after capture
+                self.optim.step_scheduled(c_adam, tabs, adam_step + 1)
+                c_adam.add_(1)
+                c_it.add_(1)
+                progress.data.copy_(ptab.index_select(0, c_it.long()).view(()))
+                if fix_first:
+                    self.graph.warp_param.weight.data[0] = 0
             for k in list(loss.keys()):
                 if torch.is_tensor(loss[k]):
                     loss[k] = loss[k].detach()
             self._drop_autograd(v)
-            self._step_graph = (g, v, loss)
-        g, v, loss = self._step_graph
-        g.replay()
-        return v, loss
+            self.graph.it = it0
+            cap = self._step_graph = dict(graph=g, var=v, loss=loss, ident=ident, limit=limit, counters=(c_adam, c_it),
+                                          tables=(tabs, ptab), adam_step=adam_step)
+        elif cap["ident"] != ident:
+            raise RuntimeError("captured_step: the graph was recorded for another batch (var.idx / images / "
+                               "parameters changed); build a new Model step or turn opt.cuda_graph off")
+        cap["graph"].replay()
+        cap["adam_step"] += 1
+        self.graph.it += 1  # Graph.compute_loss's counter (model/planar.py:379), not run on a replay
+        self.optim.advance_steps()
+        return cap["var"], cap["loss"]
 
     @staticmethod
     def _drop_autograd(var):
@@ -329,7 +374,8 @@ class Model(torch.nn.Module):
         # the edge term is evaluated every step, as the reference's Graph.forward does
         # (model/planar.py:336, 366-369): it carries no gradient, but loss.render / loss.all hold it
         self.graph.need_edges = bool(self.opt.use_edges)
-        if self.opt.get("cuda_graph") and self.graph_capable():
+        captured = bool(self.opt.get("cuda_graph")) and self.graph_capable()
+        if captured:  # the whole iteration, optimizer, progress and fix_first included
             var, loss = self.captured_step(var)
             if log_now:
                 self.summarize_loss({k: v for k, v in loss.items() if k != "all"})  # the NaN / Inf asserts
@@ -339,10 +385,10 @@ class Model(torch.nn.Module):
             loss = self.graph.compute_loss(var, mode="train")
             loss = self.summarize_loss(loss)
             loss.all.backward()
-        self.all_reduce_grads()
-        self.optim.step()
-        if self.sched:
-            self.sched.step()
+            self.all_reduce_grads()
+            self.optim.step()
+            if self.sched:
+                self.sched.step()
         if log_now:
             self.log_scalars(loss, var, step=self.it + 1, split="train")
         if (self.it + 1) % self.opt.freq.vis == 0:
@@ -352,7 +398,8 @@ class Model(torch.nn.Module):
             loader.set_postfix(it=self.it, loss=f"{float(loss.all):.3f}")
         self.timer.it = time.time() - t_start
         self.timer.it_mean = self.timer.it if self.timer.it_mean is None else 0.99 * self.timer.it_mean + 0.01 * self.timer.it
-        self.graph.neural_image.progress.data.fill_(self.it / self.opt.max_iter)
+        if not captured:  # (the captured iteration updated it on the device)
+            self.graph.neural_image.progress.data.fill_(self.it / self.opt.max_iter)
         return loss
 
     @torch.no_grad()

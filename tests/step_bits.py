@@ -53,13 +53,14 @@ def _opt(out, **over):
     return opt
 
 
-def build_case(case, out="/tmp/marf_bits"):
-    """The bf16x3 product model of `case` and its var bundle (seeded; identical on every run)."""
+def build_case(case, out="/tmp/marf_bits", precision="bf16x3"):
+    """The product model of `case` (bf16x3 unless precision says otherwise) and its var bundle
+    (seeded; identical on every run)."""
     from model import planar
     from util import EasyDict as edict
     if CASES[case] is None:
         imgs = np.load(os.path.join(GOLDEN, "cat_batch3_c1.npz"), allow_pickle=False)
-        opt = _opt(out)
+        opt = _opt(out, precision=precision)
         torch.manual_seed(3)
         m = planar.Model(opt)
         rgb = torch.from_numpy(imgs["rgb"].astype(np.float32) / np.float32(255)).to(DEV)
@@ -68,7 +69,7 @@ def build_case(case, out="/tmp/marf_bits"):
         m.build_networks()
     else:
         B, crop, L, hidden = CASES[case]
-        opt = _opt(out, H=512, W=512, patch_H=crop, patch_W=crop, batch_size=B, use_edges=False,
+        opt = _opt(out, H=512, W=512, patch_H=crop, patch_W=crop, batch_size=B, use_edges=False, precision=precision,
                    arch={"layers": [None] + list(hidden) + [3], "skip": [], "posenc": {"L_2D": L}})
         torch.manual_seed(3)
         m = planar.Model(opt)

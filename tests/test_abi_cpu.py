@@ -141,3 +141,38 @@ def test_bench_traffic_only_from_the_loaded_library(lib, tmp_path, monkeypatch):
     entry["source_hash"] = "0" * 40
     (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({"c3/bf16x3": entry}))
     assert bench.pmc_traffic("c3", "bf16x3", "mlp_step", "k_step2") is None     # another build
+
+
+def test_fp16x2_recipe_planning(lib):
+    """MARF_FP16X2 (the fp16-forward split recipe, k_step2h): full-width nets at L = 8..16 plan the
+    two-set kernel with the same parameter layout as every recipe; other nets are refused at
+    creation with the reason (no silent fallback to another kernel or recipe)."""
+    import marf_hip
+    for L in (8, 10, 13, 16):
+        n = marf_hip.Net([2 + 4 * L, 256, 256, 256, 256, 3], L, marf_hip.MARF_FP16X2)
+        assert n.step_kernel == "k_step2h", L
+        assert n.layer_spans == marf_hip.Net([2 + 4 * L, 256, 256, 256, 256, 3], L, marf_hip.MARF_BF16X3).layer_spans
+    for dims, L in (([34, 64, 64, 3], 8), ([18, 256, 256, 256, 256, 3], 4), ([66, 256, 128, 256, 256, 3], 16),
+                    ([66, 256, 256, 256, 3], 16)):
+        with pytest.raises(RuntimeError, match="fp16x2"):
+            marf_hip.Net(dims, L, marf_hip.MARF_FP16X2)
+
+
+def test_adam_schedule_matches_the_step_scalars(lib):
+    """marf_adam_schedule (the device table a captured iteration's Adam reads, host only): row k-1
+    = (lr / (1 - beta1^k), sqrt(1 - beta2^k)) in float64, rounded to float32 -- torch.optim.Adam's
+    python-float bias corrections (model/planar.py:98-99), as marf_adam_step computes them."""
+    import ctypes
+    import math
+    import numpy as np
+    n = 3000
+    buf = (ctypes.c_float * (2 * n))()
+    assert lib.marf_adam_schedule(ctypes.c_double(1e-3), ctypes.c_double(0.9), ctypes.c_double(0.999),
+                                  ctypes.c_longlong(1), ctypes.c_longlong(n), buf) == 0
+    got = np.ctypeslib.as_array(buf).reshape(n, 2)
+    for k in (1, 2, 3, 10, 100, 2999, 3000):
+        ss = np.float32(1e-3 / (1 - 0.9 ** k))
+        b2 = np.float32(math.sqrt(1 - 0.999 ** k))
+        assert got[k - 1, 0] == ss and got[k - 1, 1] == b2, k
+    assert lib.marf_adam_schedule(ctypes.c_double(1e-3), ctypes.c_double(0.9), ctypes.c_double(0.999),
+                                  ctypes.c_longlong(0), ctypes.c_longlong(1), buf) != 0

@@ -1,0 +1,208 @@
+"""The fp16x2 recipe (include/marf.h MARF_FP16X2, opt.precision "fp16x2"): k_step2h, the fused step
+with an fp16 forward -- weights fp16 hi + lo, activations single fp16, W_hi a + W_lo a (2 MFMAs per
+MAC) -- over TWO pixel sets per pass of the forward weight stages, and the split recipe's bf16
+dgrad, saved tensors and weight gradients.
+
+Bounds (north_star bf16: rgb within 1e-2, gradients within 1e-2), against oracle.PlanarStep (rgb,
+loss) and the reference's ops in float64 (gradients, tests/test_gpu_parity.py _compare_step):
+  * rgb <= 1e-2 abs (measured ~1e-3: fp16 operands carry 11 significant bits);
+  * every MLP gradient and d warp within 1e-2 of its max, cosine >= 0.999.
+Structure: reruns bit-identical, d loss x 2 -> every gradient x 2 exactly, per-pixel results
+independent of how a block pairs its tiles (the second set of a block's last group may be missing).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from test_gpu_parity import DEV, _compare_step, _err, _synthetic_setup, make_opt, one_step_grads, t
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import marf_hip
+    marf_hip.lib()
+    yield
+
+
+# (patches, crop, L, hidden): c3x2 -- the C3 net, an even tile count; c3x3 -- an odd count (a block
+# ends on a group with one set); c1 -- the C1 net (L = 8, the (3, 2) instantiation) on 128 crops;
+# L10 / L13 -- the (4, 2) and (5, 2) instantiations
+SHAPES = dict(c3x2=(2, 256, 16, [256] * 4), c3x3=(3, 256, 16, [256] * 4), c1=(5, 128, 8, [256] * 4),
+              L10=(3, 128, 10, [256] * 4), L13=(2, 128, 13, [256] * 4))
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_fp16x2_step_vs_oracle(shape, tmp_path):
+    m, var, inputs = _synthetic_setup("fp16x2", tmp_path, *SHAPES[shape])
+    assert m.graph.neural_image.engine(torch.device(DEV)).net.step_kernel == "k_step2h"
+    o = _compare_step(m, var, inputs, "fp16x2", 5)
+    assert o["rgb"] <= 1e-2 and o["loss"] <= 1e-2, o
+    assert o["grad_err"] <= 1e-2 and o["grad_cos"] >= 0.999, o
+    assert o["dh_err"] <= 1e-2 and o["dh_cos"] >= 0.999, o
+
+
+def test_fp16x2_refuses_other_nets(tmp_path):
+    """k_step2h has compile-time layer-0 instantiations only: a net that is not full width (or
+    L < 8) is refused at creation with the reason, not run on another kernel."""
+    import marf_hip
+    for dims, L in (([34, 64, 64, 3], 8), ([66, 256, 256, 256, 256, 3], 4), ([66, 256, 128, 256, 256, 3], 16)):
+        with pytest.raises(RuntimeError, match="fp16x2"):
+            marf_hip.Net(dims, L, marf_hip.MARF_FP16X2)
+
+
+@pytest.mark.parametrize("grid", [255, 7, 1])
+def test_fp16x2_tile_grouping_invariance(grid, tmp_path):
+    """k_step2h runs each block's tiles in pairs through the forward and the dgrad; a block with an
+    odd tile count ends on a group whose second set is missing (it repeats the first set's inputs
+    and stores into the sink rows).  With 255, 7 and 1 blocks instead of one per CU: rgb, the
+    hidden- and first-layer weight gradients and d warp bit-identical; the last layer's gradients and
+    the loss (block-partial sums) to summation order."""
+    from model import planar
+    from util import EasyDict as edict
+    B = 3
+    opt = make_opt(tmp_path, H=512, W=512, patch_H=256, patch_W=256, batch_size=B, precision="fp16x2",
+                   arch={"layers": [None, 256, 256, 256, 256, 3], "skip": [], "posenc": {"L_2D": 16}})
+    torch.manual_seed(0)
+    graph = planar.Graph(opt).to(DEV)
+    graph.neural_image.progress.data.fill_(0.2)
+    rng = np.random.default_rng(5)
+    gt = t(rng.random((B, 3, 256, 256)).astype(np.float32))
+    mask = t((rng.random((B, 1, 256, 256)) < 0.85).astype(np.float32))
+    var = edict(images=edict(rgb=gt, masks=mask, masks_eroded=mask, edges=None))
+    graph.need_edges = False
+    with torch.no_grad():
+        graph.warp_param.weight.copy_(t((rng.standard_normal((B, 8)) * 0.01).astype(np.float32)))
+
+    def run():
+        for q in graph.parameters():
+            q.grad = None
+        v = graph.forward(var)
+        loss = graph.compute_loss(v).rgb
+        loss.backward()
+        return (float(loss.detach()), v.rgb_prediction.detach().clone(),
+                [q.grad.clone() for q in graph.neural_image.mlp.parameters()], graph.warp_param.weight.grad.clone())
+
+    l0, rgb0, g0, w0 = run()
+    os.environ["MARF_STEP2_GRID"] = str(grid)
+    try:
+        l1, rgb1, g1, w1 = run()
+    finally:
+        del os.environ["MARF_STEP2_GRID"]
+    assert torch.equal(rgb0, rgb1)
+    assert torch.equal(w0, w1)
+    for i, (a, b) in enumerate(zip(g0[:-2], g1[:-2])):
+        assert torch.equal(a, b), (i, (a - b).abs().max().item())
+    for a, b in zip(g0[-2:], g1[-2:]):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-7 * float(a.abs().max())), (a - b).abs().max().item()
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+
+
+def test_fp16x2_headline_step():
+    """The headline size (BASELINE C3: 64 patches x 256x256, L = 16, 66-256x4-3) on k_step2h:
+    reruns bit-identical, d loss x 2 -> every gradient x 2 exactly, rgb of 512 sampled pixels of
+    every patch within 1e-2 of the oracle's fp32 forward, d warp of two patches within 1e-2 of the
+    float64 reference ops with cosine >= 0.999, and the step's gradients against the bf16x3 recipe's
+    (the same dgrad arithmetic on a different forward) at cosine >= 0.999."""
+    import cpu_ref
+    import step_bits
+    m, var = step_bits.build_case("c3x64", precision="fp16x2")
+    eng = m.graph.neural_image.engine(torch.device(DEV))
+    assert eng.net.step_kernel == "k_step2h" and m.batch_size == 64
+    params = [(l.weight.detach().cpu().numpy().copy(), l.bias.detach().cpu().numpy().copy()) for l in m.graph.neural_image.mlp]
+    warp = m.graph.warp_param.weight.detach().cpu().numpy().copy()
+    rgb_t = m.images.rgb.cpu().numpy()
+    mask_t = m.images.masks.cpu().numpy()
+
+    def step(model, scale):
+        model.optim.zero_grad()
+        v = model.graph.forward(var, mode="train")
+        loss = model.summarize_loss(model.graph.compute_loss(v, mode="train"))
+        (loss.all * scale).backward()
+        return (v.rgb_prediction.detach().clone(), float(loss.rgb), model.graph.warp_param.weight.grad.detach().clone(),
+                [p.grad.detach().clone() for p in model.graph.neural_image.mlp.parameters()])
+
+    rgb1, l1, dh1, g1 = step(m, 1.0)
+    rgb2, l2, dh2, g2 = step(m, 1.0)
+    _, l3, dh3, g3 = step(m, 2.0)
+    assert torch.equal(rgb1, rgb2) and l1 == l2 == l3 and torch.equal(dh1, dh2)
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+    assert torch.equal(2 * dh1, dh3) and all(torch.equal(2 * a, b) for a, b in zip(g1, g3))
+    assert all(torch.isfinite(a).all() for a in g1) and torch.isfinite(dh1).all()
+
+    rng = np.random.default_rng(11)
+    idx = np.sort(rng.choice(256 * 256, 512, replace=False))
+    xy = oracle.pixel_grid(512, 512, 256, 256)[idx]
+    Hm = oracle.sl3_to_SL3(warp)
+    uv = oracle.warp_points(np.ascontiguousarray(np.broadcast_to(xy, (64,) + xy.shape)), Hm)
+    f0 = oracle.posenc_features(uv, 16, oracle.c2f_weights(np.float32(0.2), [0, 0.4], 16)).reshape(-1, 66)
+    ref_rgb = oracle.mlp_forward(f0, params)[1].reshape(64, 512, 3)
+    err = float(np.abs(rgb1.cpu().numpy()[:, idx] - ref_rgb).max())
+    print(f"fp16x2 C3 headline: rgb max |err| over 64 x 512 pixels {err:.3g}")
+    assert err <= 1e-2, err
+
+    sel = [17, 50]
+    cfg = dict(H=512, W=512, patch_H=256, patch_W=256, L=16, c2f=[0, 0.4], max_iter=3000, lr=1e-3, lr_warp=1e-3,
+               fix_first=True, use_edges=False, alpha_initial=0.0, alpha_final=1.0)
+    scale = float(mask_t[sel].sum(dtype=np.float64) / mask_t.sum(dtype=np.float64))
+    cpu_ref.set_threads()
+    s = cpu_ref.CpuRefStep(cfg, params, warp[sel], rgb_t[sel], mask_t[sel], dtype=torch.float64, device=DEV)
+    s.progress.data.fill_(0.2)
+    truth = np.asarray(s.step()["dh"], np.float64) * scale
+    ours = dh1.cpu().numpy()[sel]
+    e = _err(ours, truth)
+    c = float(ours.ravel() @ truth.ravel() / (np.linalg.norm(ours) * np.linalg.norm(truth)))
+    print(f"fp16x2 C3 headline: d warp of patches {sel}: error {e:.3g}, cosine {c:.6f}")
+    assert e <= 1e-2 and c >= 0.999, (e, c)
+
+    # the same state in the bf16x3 recipe: the dgrad arithmetic is shared, the forward differs
+    m3, _ = step_bits.build_case("c3x64", precision="bf16x3")
+    _, _, dh_x3, g_x3 = step(m3, 1.0)
+    cos = [float((a.double().ravel() @ b.double().ravel()) / (a.double().norm() * b.double().norm()))
+           for a, b in zip(g1, g_x3)]
+    print("fp16x2 vs bf16x3 gradient cosines:", [round(x, 6) for x in cos])
+    assert min(cos) >= 0.999, cos
+
+
+@pytest.mark.parametrize("prog", [0.0, 0.5])
+def test_fp16x2_render_vs_reference(prog, tmp_path):
+    """predict_entire_image (model/planar.py:211-217) in the fp16x2 recipe: the seed-3 init on the
+    unwarped 360x480 canvas through k_step2h's forward stages only (marf_render, explicit
+    coordinates), every 37th pixel against the reference golden within 1e-2 abs (north_star bf16)."""
+    from test_gpu_parity import c1_setup, g
+    z = g("api")
+    m, _ = c1_setup("fp16x2", tmp_path)
+    m.graph.neural_image.progress.data.fill_(prog)
+    img = m.predict_entire_image()
+    assert tuple(img.shape) == (3, 360, 480)
+    got = img.permute(1, 2, 0).reshape(-1, 3).numpy()[z["pred_idx"]]
+    err = float(np.abs(got - z[f"pred_p{prog}_sample"]).max())
+    print(f"fp16x2 render p={prog}: max |err| {err:.3g}")
+    assert err <= 1e-2, err
+
+
+def test_fp16x2_training_steps_track_fp32(tmp_path):
+    """Ten Model.train_iteration calls on the cat_batch3 C1 problem (seed 3) in fp16x2 and in fp32
+    from the same init: per-step losses within 1e-3 relative and warps within 1e-3 absolute (the
+    recipes' rounding differs from the first step; the trajectories stay together)."""
+    from test_gpu_parity import c1_setup, _Loader
+    out = {}
+    for prec in ("fp16x2", "fp32"):
+        m, var = c1_setup(prec, tmp_path)
+        m.opt.freq.vis = 10 ** 9
+        losses = []
+        for _ in range(10):
+            loss = m.train_iteration(var, _Loader())
+            m.graph.warp_param.weight.data[0] = 0
+            losses.append(float(loss.rgb))
+        out[prec] = (np.array(losses), m.graph.warp_param.weight.detach().cpu().numpy())
+    dl = np.abs(out["fp16x2"][0] / out["fp32"][0] - 1).max()
+    dw = np.abs(out["fp16x2"][1] - out["fp32"][1]).max()
+    print(f"fp16x2 vs fp32 over 10 steps: loss rel {dl:.3g}, warps {dw:.3g}")
+    assert dl <= 1e-3 and dw <= 1e-3, (dl, dw)

@@ -2,8 +2,9 @@
 the pre-decoded cat_batch3 inputs (--dataset_npz), seed 3, c2f [0, 0.4], the full 3000 iterations
 (progress = it / max_iter drives the c2f schedule, so a shorter run is a different experiment) in
 the benchmarked bf16x3 recipe and in fp32, frames every 100 iterations.  Checks that the run
-completes, writes its options, scalar log and frames, and that the final logged PSNR is within
-0.05 dB of the reference's 25.9968 dB."""
+completes, writes its options, scalar log and frames, and that the final logged PSNR and the mean of
+the last 10 logged values are each within 0.05 dB of the nearest of the reference's own three runs
+(tests/psnr_rule.py)."""
 import json
 import os
 import subprocess
@@ -11,6 +12,7 @@ import sys
 
 import pytest
 
+import psnr_rule
 from conftest import GOLDEN, PKG
 
 pytestmark = pytest.mark.gpu
@@ -37,4 +39,7 @@ def test_train_py_dataset_npz(precision, tmp_path):
     frames = sorted(int(f.split(".")[0]) for f in os.listdir(out / "vis"))  # frame 0 + one per 100 iterations
     assert frames == list(range(31)), frames
     print(precision, {k: round(v, 3) for k, v in sorted(psnr.items()) if k % 300 == 0})
-    assert abs(psnr[3000] - 25.9968) <= 0.05, psnr[3000]
+    last10 = [psnr[k] for k in sorted(psnr)[-10:]]
+    ok, msg = psnr_rule.psnr_check(psnr[3000], sum(last10) / 10)
+    print(precision, msg)
+    assert ok, msg

@@ -48,3 +48,23 @@ def test_lin_comb_all_zero_terms_keep_the_plain_result():
     assert lin_comb([(1.0, z), (0.5, z)]) == 0
     r = lin_comb([(1.0, z)], start_zero=True)
     assert float(r) == 0.0
+
+
+def test_psnr_rule_nearest_reference_run():
+    """The seed-3 PSNR rule (tests/psnr_rule.py): final and mean of the last 10 logged values within
+    0.05 dB of the nearest of the reference's own three runs.  Each reference run passes it against
+    the set (the single-anchor rule failed the one-ulp rerun: 26.0868 vs 25.9968), the split-dz
+    recipe's seed-3 run (26.086 dB final) passes, and runs outside the band fail."""
+    import psnr_rule
+    runs = psnr_rule.reference_runs()
+    assert [r[0] for r in runs] == ["survey", "base", "ulp1"]
+    assert abs(runs[0][1] - 25.9968) < 1e-9 and abs(runs[1][1] - 26.0499) < 1e-4 and abs(runs[2][1] - 26.0868) < 1e-4
+    for _, final, mean10 in runs[1:]:
+        assert psnr_rule.psnr_check(final, mean10)[0]
+    m_ulp1 = runs[2][2]
+    assert psnr_rule.psnr_check(26.086, m_ulp1)[0]
+    assert psnr_rule.psnr_check(25.9968, m_ulp1)[0]
+    assert not psnr_rule.psnr_check(25.93, m_ulp1)[0]    # below every final by > 0.05
+    assert not psnr_rule.psnr_check(26.14, m_ulp1)[0]    # above every final by > 0.05
+    assert not psnr_rule.psnr_check(26.05, 25.95)[0]     # the trajectory mean off the band
+    assert not psnr_rule.psnr_check(24.9, 24.9)[0]       # the other basin

@@ -43,6 +43,12 @@ for k, cs in vals.items():
         row["hbm_write_bytes"] = row["WRITE_SIZE"] * 1024
     if dur.get(k):
         row["pmc_avg_ns"] = sum(dur[k]) / len(dur[k])
+    # matrix-core utilisation (MI355X_MICROARCH.md: SQ_VALU_MFMA_BUSY_CYCLES counts cycles summed over
+    # the SIMDs; GRBM_GUI_ACTIVE is summed over the 8 XCDs: / 8 = the dispatch's wall cycles; 1024 SIMDs)
+    if row.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in row:
+        row["mfma_busy"] = row["SQ_VALU_MFMA_BUSY_CYCLES"] / (row["GRBM_GUI_ACTIVE"] / 8 * 1024)
+    if row.get("SQ_INSTS_MFMA") and "SQ_INSTS_VALU" in row:
+        row["valu_per_mfma"] = row["SQ_INSTS_VALU"] / row["SQ_INSTS_MFMA"]
     rows.append(row)
 cols = sorted({c for r in rows for c in r if c != "kernel"})
 out = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else None
@@ -88,8 +94,14 @@ if "--traffic" in sys.argv:
                     continue
             kernels[name] = {"symbol": k, "hbm_read_bytes": r["hbm_read_bytes"], "hbm_write_bytes": r["hbm_write_bytes"],
                              "pmc_avg_ns": r.get("pmc_avg_ns")}
+            for c in ("mfma_busy", "valu_per_mfma", "SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD",
+                      "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"):
+                if c in r:
+                    kernels[name][c] = r[c]
     data[tag] = {"source_hash": src_hash, "kernels": kernels,
-                 "source": (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 2 ({root}); "
-                            "read bytes = 2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md HBM)")}
+                 "source": (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (+ SQ_INSTS_VALU SQ_INSTS_MFMA "
+                            f"SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE) passes over bench.py --steps 2 ({root}); "
+                            "read bytes = 2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md HBM); mfma_busy = "
+                            "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)")}
     json.dump(data, open(tj, "w"), indent=1)
     print("wrote", tj)
