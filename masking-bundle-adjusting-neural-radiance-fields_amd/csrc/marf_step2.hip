@@ -185,6 +185,12 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
     constexpr bool FIX = NK0F > 0;
     static_assert(NK0F <= C::NK0, "layer-0 k-steps");
     static_assert(!HF || (SPLIT && !DZ && NK0F > 0 && NS == 2), "fp16x2: split dgrad, two sets, compile-time layer 0");
+    // the hidden dgrad of a group's two pixel sets in one pass per weight stage (compile-time nets;
+    // MARF_STEP2_J2=0 at build time keeps one pass per set for A/B)
+#ifndef MARF_STEP2_J2
+#define MARF_STEP2_J2 1
+#endif
+    constexpr bool J2 = MARF_STEP2_J2 && NS == 2 && SPLIT && !SDZ && FIX;
     constexpr int R0Q = NKH / (FIX ? NK0F : NKH);  // layer-0 row tiles per stage (the host's r0)
     constexpr int R0F = R0Q < 1 ? 1 : (R0Q > NRT ? NRT : R0Q);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -741,17 +747,26 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
     // MFMAs), each A fragment read from LDS once for the two sets.  Per k-step the order is (set 0,
     // hi), (set 1, hi), (set 0, lo), (set 1, lo): each set's chain is hi, lo per k-step, as one set
     // alone would run it.  hook(ks, p) runs in the gap after MFMA p (0..3) of k-step ks.
+    // (F16 = false: the same pass in bf16 -- the split dgrad of two pixel sets, W_hi^T dz + W_lo^T dz
+    //  per set in the split recipe's order, so the same bits as one GEMM pass per set)
     auto gemm2 = [&](f32x16& c0, f32x16& c1, const char* slot, const S2Frag* B0, const S2Frag* B1, auto nk_tag,
-                     auto&& hook, auto pieces_tag) {
+                     auto&& hook, auto pieces_tag, auto f16_tag) {
         constexpr int NK = decltype(nk_tag)::value;
+        constexpr bool F16 = decltype(f16_tag)::value;
         typedef std::integral_constant<int, 0> P0;
         typedef std::integral_constant<int, 1> P1;
         typedef std::integral_constant<int, 2> P2;
         typedef std::integral_constant<int, 3> P3;
-        const f16x8* ah = reinterpret_cast<const f16x8*>(slot + lane * 16);
-        const f16x8* al = reinterpret_cast<const f16x8*>(slot + C::LO + lane * 16);
+        auto mma = [&](f32x16& c, const uint4& av, const S2Frag& b) {
+            if constexpr (F16)
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, av), b.h, c, 0, 0, 0);
+            else
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av), b.f, c, 0, 0, 0);
+        };
+        const uint4* ah = reinterpret_cast<const uint4*>(slot + lane * 16);
+        const uint4* al = reinterpret_cast<const uint4*>(slot + C::LO + lane * 16);
         constexpr int P = NK < 4 ? NK : 4;
-        f16x8 A0[4], A1[4];
+        uint4 A0[4], A1[4];
 #pragma unroll
         for (int u = 0; u < P; ++u) {
             A0[u] = ah[u * 64];
@@ -762,23 +777,25 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             constexpr int u = ks & 3;
             constexpr bool refill = ks + P < NK;
             __builtin_amdgcn_sched_barrier(0);
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0[u], B0[ks].h, c0, 0, 0, 0);
+            mma(c0, A0[u], B0[ks]);
             hook(ksc, P0());
             __builtin_amdgcn_sched_barrier(0);
-            c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0[u], B1[ks].h, c1, 0, 0, 0);
+            mma(c1, A0[u], B1[ks]);
             hook(ksc, P1());
             if constexpr (refill) A0[u] = ah[(ks + P) * 64];
             __builtin_amdgcn_sched_barrier(0);
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1[u], B0[ks].h, c0, 0, 0, 0);
+            mma(c0, A1[u], B0[ks]);
             hook(ksc, P2());
             __builtin_amdgcn_sched_barrier(0);
-            c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1[u], B1[ks].h, c1, 0, 0, 0);
+            mma(c1, A1[u], B1[ks]);
             hook(ksc, P3());
             if constexpr (refill) A1[u] = al[(ks + P) * 64];
             piece_at(ksc, nk_tag, pieces_tag);
             __builtin_amdgcn_sched_barrier(0);
         });
     };
+    typedef std::integral_constant<bool, true> F16t;
+    typedef std::integral_constant<bool, false> BF16t;
     // epilogue of a 32-row accumulator tile of set s, per pair q of registers (2q, 2q + 1): ReLU of
     // both (integer max with 0, as frelu), the fp16 operand pair into the next layer's fragment
     // (k-step 2 rt + q / 4, word q mod 4), the bf16 pair for the saved tensor, its ReLU mask bits
@@ -1013,14 +1030,14 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                         st_cur += 2;
                     }
                     if constexpr (rt == 0) {
-                        gemm2(c0, c1, slot, B0, B1, nk_tag, nohook, PcL());
+                        gemm2(c0, c1, slot, B0, B1, nk_tag, nohook, PcL(), F16t());
                     } else {
                         typedef std::integral_constant<int, rt - 1> RP;
                         e2[0].bits = 0;
                         e2[1].bits = 0;
                         gemm2(c0, c1, slot, B0, B1, nk_tag, [&](auto ksc, auto pc) {
                             hook2(q0, q1, Oh, Ol, RP(), ksc, pc, ppk_tag);
-                        }, PcL());
+                        }, PcL(), F16t());
                         free_pairs(q0, q1, Oh, Ol, RP(), std::integral_constant<int, PPK * NK>());
                         ffinish2(l, RP(), I0(), save, srow[0], false);
                         ffinish2(l, RP(), I1(), save, srow[1], false);
@@ -1050,7 +1067,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                 c0 = bias_init(ly_int(nl - 1, 2), 0);
                 c1 = c0;
                 const char* slot = stage_begin(false);
-                gemm2(c0, c1, slot, Bh, Bl, NKHt(), nohook, PcOn());
+                gemm2(c0, c1, slot, Bh, Bl, NKHt(), nohook, PcOn(), F16t());
                 s2_sfor<2>([&](auto sc) {
                     constexpr int sset = decltype(sc)::value;
                     const f32x16& acc = sset ? c1 : c0;
@@ -1118,12 +1135,17 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                             gts[(4 + c) * 32 + pxl] = f2h(gs - h2f(hi));
                         }
                     }
+                    // (a compiler barrier: the u16 stores and the f16x8 load below do not alias under
+                    //  type-based alias analysis, and without it the second set reused the first set's
+                    //  load of the image)
+                    asm volatile("" ::: "memory");
                     const f16x8 ga = *reinterpret_cast<const f16x8*>(gts + (lane & 15) * 32 + 8 * (lane >> 4));
                     const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
                     const S2Frag* Bf = sset ? Bl : Bh;
 #pragma unroll
                     for (int ks = 0; ks < NKH; ++ks) {
                         *reinterpret_cast<uint4*>(trs + (pxl * 2 + h) * 8) = Bf[ks].u;
+                        asm volatile("" ::: "memory");
                         const u16* b0 = trs + (8 * gq + q) * 16 + (pp & 1) * 8 + 4 * (pp >> 1);
                         i16x4 vv[2] = {s2_tr16(b0), s2_tr16(b0 + 4 * 16)};
                         const f32x4 r4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ga, *reinterpret_cast<f16x8*>(vv), (f32x4){}, 0, 0, 0);
@@ -1535,6 +1557,53 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             s2_sfor<NS>([&](auto sc) {
                 brow[decltype(sc)::value] = ly_ptr(l, 1) + (sl0[decltype(sc)::value] >> 5) * ly_int(l, 4) * 32 + pxl * 16 + 8 * h;
             });
+            if constexpr (J2) {
+                // both sets in ONE pass per stage (gemm2, bf16): each A fragment read from LDS once for
+                // the two sets; per set the MFMA sequence, epilogue and stores of the per-set passes
+                // below, so the same bits.  The epilogue of row tile rt-1 of both sets (set 0 in
+                // k-steps 0-7, set 1 in 8-15) runs in the gaps of row tile rt.
+                EpSt ebs[2];
+                s2_sfor<NRT>([&](auto rtc) {
+                    constexpr int rt = decltype(rtc)::value;
+                    f32x16& c0 = hacc[(rt & 1) ? 2 : 0];
+                    f32x16& c1 = hacc[(rt & 1) ? 3 : 1];
+                    f32x16& q0 = hacc[(rt & 1) ? 0 : 2];
+                    f32x16& q1 = hacc[(rt & 1) ? 1 : 3];
+                    const char* slot = stage_begin(false);
+                    c0 = (f32x16){};
+                    c1 = (f32x16){};
+                    if constexpr (rt == 0) {
+                        S2T_BEGIN(9);
+                        gemm2(c0, c1, slot, Dh[0], Dh[1], NKHt(), nohook, PcOn(), BF16t());
+                        S2T_END(9);
+                    } else {
+                        typedef std::integral_constant<int, rt - 1> RP;
+                        ebs[0].mw = mks_b(0)[(lmask * C::NMW + ((rt - 1) >> 1)) * 64 + lane];
+                        ebs[1].mw = mks_b(1)[(lmask * C::NMW + ((rt - 1) >> 1)) * 64 + lane];
+                        S2T_BEGIN(9);
+                        gemm2(c0, c1, slot, Dh[0], Dh[1], NKHt(), [&](auto ksc, auto pc) {
+                            constexpr int ks = decltype(ksc)::value, p = decltype(pc)::value;
+                            if constexpr (p < 2) {
+                                constexpr int sset = ks >> 3;
+                                bstep(ebs[sset], sset ? q1 : q0, std::integral_constant<int, 2 * (ks & 7) + p>(), RP());
+                            }
+                        }, PcOn(), BF16t());
+                        S2T_END(9);
+                        S2T_BEGIN(11);
+                        bfinish(ebs[0], Do[0], RP(), brow[0]);
+                        bfinish(ebs[1], Do[1], RP(), brow[1]);
+                        S2T_END(11);
+                    }
+                    if constexpr (rt == NRT - 1) {
+                        ebs[0].mw = mks_b(0)[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
+                        ebs[1].mw = mks_b(1)[(lmask * C::NMW + (rt >> 1)) * 64 + lane];
+                        bsteps_free(ebs[0], c0, rtc);
+                        bsteps_free(ebs[1], c1, rtc);
+                        bfinish(ebs[0], Do[0], rtc, brow[0]);
+                        bfinish(ebs[1], Do[1], rtc, brow[1]);
+                    }
+                });
+            } else
             s2_sfor<NRT>([&](auto rtc) {
                 constexpr int rt = decltype(rtc)::value;
                 if (rt < nrt) {

@@ -240,7 +240,6 @@ class Model(torch.nn.Module):
         creates the optimizer state and records once; every call replays.  Host bookkeeping per
         replay: Graph.it, each parameter's Adam step.  The graph is bound to the batch it was
         recorded with: another var raises.  Returns (var, loss) with the graph's static tensors."""
-        ident = self._capture_ident(var)
         cap = self._step_graph
         if cap is not None and max(self.it, cap["adam_step"]) + 1 >= cap["limit"]:
             cap = self._step_graph = None  # past the recorded tables: record again with longer ones
@@ -292,9 +291,11 @@ class Model(torch.nn.Module):
                     loss[k] = loss[k].detach()
             self._drop_autograd(v)
             self.graph.it = it0
-            cap = self._step_graph = dict(graph=g, var=v, loss=loss, ident=ident, limit=limit, counters=(c_adam, c_it),
+            # (after the warm-up: the first forward moves the MLP parameters into the engine's flat buffer)
+            cap = self._step_graph = dict(graph=g, var=v, loss=loss, ident=self._capture_ident(var), limit=limit,
+                                          counters=(c_adam, c_it),
                                           tables=(tabs, ptab), adam_step=adam_step)
-        elif cap["ident"] != ident:
+        elif cap["ident"] != self._capture_ident(var):
             raise RuntimeError("captured_step: the graph was recorded for another batch (var.idx / images / "
                                "parameters changed); build a new Model step or turn opt.cuda_graph off")
         cap["graph"].replay()

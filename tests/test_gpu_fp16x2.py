@@ -52,7 +52,7 @@ def test_fp16x2_refuses_other_nets(tmp_path):
     """k_step2h has compile-time layer-0 instantiations only: a net that is not full width (or
     L < 8) is refused at creation with the reason, not run on another kernel."""
     import marf_hip
-    for dims, L in (([34, 64, 64, 3], 8), ([66, 256, 256, 256, 256, 3], 4), ([66, 256, 128, 256, 256, 3], 16)):
+    for dims, L in (([34, 64, 64, 3], 8), ([18, 256, 256, 256, 256, 3], 4), ([66, 256, 128, 256, 256, 3], 16)):
         with pytest.raises(RuntimeError, match="fp16x2"):
             marf_hip.Net(dims, L, marf_hip.MARF_FP16X2)
 

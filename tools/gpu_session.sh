@@ -11,7 +11,8 @@
 #                             alternating twice (timing-only variants: MARF_AB_TIMING_ONLY=1)
 #   envab=VAR:v1,v2[:c1,c3]   C1 / C3 benches with VAR=v1, v2, ... alternating twice (library A/B switches)
 #   cfg                       secondary bench lines (tools/bench_configs.sh)
-#   pmc=<config>/<precision>  FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh)
+#   pmc=<config>/<precision>  FETCH_SIZE / WRITE_SIZE / matrix-core passes (tools/pmc_traffic.sh)
+#   basin=<draws>:<n>=<recipe>;...  seed-3 C1 basin rates over one-ulp init draws (tools/basin_table.py)
 # Every GPU step has its own time limit; the session stops at the first failure, abort or timeout.
 set -o pipefail
 TAG=$1; shift
@@ -83,6 +84,16 @@ for step in "$@"; do
     pmc=*)
       C=${step#pmc=}
       bash tools/pmc_traffic.sh $TAG/pmc_${C%/*} ${C%/*} ${C#*/} || exit 1 ;;
+    basin=*)
+      # basin=<draws>:<name>=<recipe>[;<name>=<recipe>...]  the seed-3 C1 3000-step run over one-ulp
+      # init draws per recipe (tools/basin_table.py; a recipe = precision[:VAR=value,...]) ->
+      # <tag>/basin/table.json.  The committed basin table (profiles/basin_table.json) is the
+      # merge of these runs: e.g. basin=25-144:fp32=fp32;bf16x3=bf16x3;fp16x2=fp16x2
+      SPEC=${step#basin=}; DRAWS=${SPEC%%:*}; IFS=';' read -ra RS <<< "${SPEC#*:}"
+      timeout -k 10 ${BASIN_TIMEOUT:-1100} python -u tools/basin_table.py --draws $DRAWS --workers ${BASIN_WORKERS:-4} \
+        --chunk ${BASIN_CHUNK:-5} --deadline ${BASIN_DEADLINE:-800} --hard-deadline ${BASIN_HARD:-1000} --out $OUT/basin "${RS[@]}" > $OUT/basin.log 2>&1
+      RC=$?; tail -6 $OUT/basin.log
+      [ $RC = 0 ] || { echo "basin exit $RC: stopping"; exit $RC; } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
