@@ -984,14 +984,14 @@ def test_c1_3000_iterations_psnr_and_warps(precision, tmp_path):
 
 # ------------------------------------------------------------------------ C3 / C5 shapes vs the oracle
 
-def _synthetic_setup(precision, tmp_path, B, crop, L, hidden, c2f=(0, 0.4), progress=0.2, seed=3):
+def _synthetic_setup(precision, tmp_path, B, crop, L, hidden, c2f=(0, 0.4), progress=0.2, seed=3, skip=()):
     """A C3- or C5-shaped graph (512x512 canvas, crop x crop patches, L bands, hidden widths) with
     seeded procedural targets, Bernoulli(0.85) masks and non-zero warps on every patch.  Returns
     the product's model, its var bundle and the inputs / config for the CPU checkers."""
     from model import planar
     from util import EasyDict as edict
     opt = make_opt(tmp_path, H=512, W=512, patch_H=crop, patch_W=crop, batch_size=B, precision=precision,
-                   use_edges=False, arch={"layers": [None] + list(hidden) + [3], "skip": [], "posenc": {"L_2D": L}},
+                   use_edges=False, arch={"layers": [None] + list(hidden) + [3], "skip": list(skip), "posenc": {"L_2D": L}},
                    barf_c2f=None if c2f is None else list(c2f))
     torch.manual_seed(seed)
     m = planar.Model(opt)
@@ -1009,7 +1009,7 @@ def _synthetic_setup(precision, tmp_path, B, crop, L, hidden, c2f=(0, 0.4), prog
     params = [(m.graph.neural_image.mlp[i].weight.detach().cpu().numpy().copy(),
                m.graph.neural_image.mlp[i].bias.detach().cpu().numpy().copy()) for i in range(len(hidden) + 1)]
     cfg = dict(H=512, W=512, patch_H=crop, patch_W=crop, L=L, c2f=None if c2f is None else list(c2f), max_iter=3000,
-               lr=1e-3, lr_warp=1e-3, fix_first=True, use_edges=False, alpha_initial=0.0, alpha_final=1.0)
+               lr=1e-3, lr_warp=1e-3, fix_first=True, use_edges=False, alpha_initial=0.0, alpha_final=1.0, skip=tuple(skip))
     return m, edict(idx=torch.arange(B), images=m.images), (cfg, params, warp, rgb, mask, progress)
 
 
@@ -1294,6 +1294,22 @@ def test_c3_headline_step():
     ref = _bits_fixture()["cases"]["c3x64"]
     bad = sorted(k for k in ref["bits"] if got["bits"].get(k) != ref["bits"][k])
     assert not bad, bad
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_wide_skip_net_8wave_step_vs_oracle(precision, tmp_path):
+    """A 16-bit skip net at the reference's width (layers [66, 256 x 4, 3], skip [2], L = 16: the
+    skip layer's input is 256 + 96 > 256 wide) runs the 8-wave, 128-pixel fused tile kernel
+    k_mlp_step<..., NW = 8, SK = true> (marf_abi.hip net planning).  One step on 2 x 64x64 patches
+    against the oracle (rgb, loss) and the reference's ops in float64 (cpu_ref with skip,
+    model/planar.py:419-420, 440-441): north_star bf16 bounds -- rgb <= 1e-2, MLP-gradient cosine
+    >= 0.99, warp-gradient cosine >= 0.98."""
+    m, var, inputs = _synthetic_setup(precision, tmp_path, 2, 64, 16, [256] * 4, skip=[2])
+    eng = m.graph.neural_image.engine(torch.device(DEV))
+    assert eng.net.step_kernel == "k_mlp_step"
+    o = _compare_step(m, var, inputs, precision, 5)
+    assert o["rgb"] <= 1e-2 and o["loss"] <= 2e-2, o
+    assert o["grad_cos"] >= 0.99 and o["dh_cos"] >= 0.98, o
 
 
 @pytest.mark.parametrize("c2f", [(0, 0.4), None], ids=["c2f", "noc2f"])
