@@ -34,7 +34,7 @@ PEAK_BF16 = 2.5e15   # dense bf16 MFMA, MI355X_MICROARCH.md
 PEAK_FP32 = 157.3e12  # fp32 MFMA = vector rate
 PEAK_HBM = 8.0e12
 RECIPES = {"bf16x3": "bf16x3 recipe (split-bf16 hi+lo MFMA operands, fp32 accumulate; seed-3 parity)",
-           "fp16x2": "fp16x2 recipe (fp16 hi+lo weights x fp16 activations forward, split-bf16 dgrad; fp32 accumulate)",
+           "fp16x2": "fp16x2 recipe (fp16 hi+lo weights x fp16 activations / dz, 2 MFMAs per MAC; fp32 accumulate)",
            "bf16": "plain bf16 MFMA (fp32 accumulate)", "fp16": "plain fp16 MFMA (fp32 accumulate)", "fp32": "fp32"}
 
 CONFIGS = {

@@ -17,8 +17,7 @@
  *     returns a thread-local message for the last failure.
  *   - float32 everywhere in the interface; dtype selects the internal MLP arithmetic
  *     (MARF_FP32 = exact fp32 MFMA, MARF_BF16 = bf16 MFMA with fp32 accumulation, MARF_BF16X3 = split
- *     bf16, MARF_FP16 = fp16 MFMA with fp32 accumulation, MARF_FP16X2 = split fp16 forward + split
- *     bf16 dgrad).
+ *     bf16, MARF_FP16 = fp16 MFMA with fp32 accumulation, MARF_FP16X2 = split-fp16 weights).
  */
 #ifndef MARF_H
 #define MARF_H
@@ -43,10 +42,11 @@ extern "C" {
 
 #define MARF_FP16 3   /* fp16 MFMA (v_mfma_f32_32x32x16_f16, fp32 accumulation): weights, activations, dz and the
                          saved tensors in IEEE binary16 (11 significant bits); the bf16 rate */
-#define MARF_FP16X2 4 /* split fp16 forward: weights as fp16 hi + lo pairs, forward activations single fp16
-                         (hi*a + lo*a: 2 MFMAs per MAC), the dgrad, dz and saved tensors as MARF_BF16X3;
-                         full-width nets (every hidden layer 256 wide, <= 5 layers, L <= 32, no skip);
-                         fused step and marf_render only */
+#define MARF_FP16X2 4 /* split-fp16 weights: every MFMA fp16 with the weights as fp16 hi + lo pairs (W_hi a +
+                         W_lo a forward, W_hi^T dz + W_lo^T dz dgrad: 2 MFMAs per MAC), activations, dz and
+                         the saved tensors single fp16 (dz carrying an exact 2^10 gradient scale); full-width
+                         nets (5 layers, every hidden layer 256 wide, 8 <= L <= 16, no skip); fused step and
+                         marf_render only */
 
 #define MARF_GEO_GRID 0   /* pixels of the centre crop, warped by a per-patch homography */
 #define MARF_GEO_COORDS 1 /* explicit [n][2] coordinates (one point set) */

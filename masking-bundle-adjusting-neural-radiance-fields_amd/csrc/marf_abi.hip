@@ -1271,6 +1271,9 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
     float* bpart = (float*)(sv + p.bpart);
     const float* denom = d_loss_out + 1;
     const int nl = net->n_layers;
+    // the saved tensors' precision (fp16x2: fp16, carrying the dgrad's 2^10 gradient scale)
+    const int sdt = q.variant == 3 ? 2 : 1;
+    const float post = q.variant == 3 ? 1.0f / 1024.0f : 1.0f;
     // The fused weight gradients (marf_launch_wgrad_fused): the hidden layers in one launch, layer 0
     // beside it on the side stream, every reduction in one launch -- the same partials and sums as
     // the per-layer launches below (bit-identical).  The layer events follow it, in the per-layer order.
@@ -1328,7 +1331,7 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                 {
                     MarfProfScope ps("wgrad_fused", s);
                     HIPCHK(marf_launch_wgrad_fused(Lf, nf, p.S, (int)chunk, n_chunks, g, (const float*)(sv + p.c2f),
-                                                   net->L, q.nk0w, d_gout, denom, s, st->s2, st->ev[0], st->ev[1]),
+                                                   net->L, q.nk0w, d_gout, denom, s, st->s2, st->ev[0], st->ev[1], sdt, post),
                            "step_backward fused weight gradients");
                 }
                 if (dh_side) {
@@ -1390,10 +1393,11 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                 MarfProfScope ps(l == 0 ? "wgrad_l0" : "wgrad_hidden", s);
                 if (l == 0 && f0)
                     HIPCHK(marf_launch_wgrad_l0_recompute(sv + p.dz[1], net->Kp[1], g, (const float*)(sv + p.c2f), net->L,
-                                                          q.nk0w, q.ldf0, p.S, net->Mp[0], (int)chunk, n_chunks, part, bpart, s),
+                                                          q.nk0w, q.ldf0, p.S, net->Mp[0], (int)chunk, n_chunks, part, bpart, s,
+                                                          nullptr, sdt),
                            "step_backward wgrad_l0 (feat_0 recomputed)");
                 else
-                    HIPCHK(marf_launch_wgrad(1, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K,
+                    HIPCHK(marf_launch_wgrad(sdt, sv + p.dz[l + 1], net->Kp[l + 1], sv + p.feat[l], K, p.S, net->Mp[l], K,
                                              (int)chunk, n_chunks, part, bpart, s, nullptr, true),
                            "step_backward wgrad");
             }
@@ -1401,7 +1405,7 @@ static int step2_backward(const marf_net* net, const marf_geometry* geo, const v
                 MarfProfScope ps("wgrad_reduce", s);
                 HIPCHK(marf_launch_wgrad_reduce(part, bpart, n_chunks, net->Mp[l], K, net->dims[l + 1], net->dims[l],
                                                 d_dparams + net->w_off[l], d_dparams + net->b_off[l], s, d_gout, denom,
-                                                nullptr, l == 0 ? kmap : nullptr),
+                                                nullptr, l == 0 ? kmap : nullptr, post),
                        "step_backward wgrad reduce");
             }
             rc = mark_layer(ev, l, s);

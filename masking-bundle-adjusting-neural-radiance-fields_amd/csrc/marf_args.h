@@ -152,7 +152,7 @@ bool marf_wgrad_range_ok(int dtype, int M, int ldz, int K, int ldf);
 bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk, int n_chunks, long long Np_pad);
 hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev& geo, const float* c2f_w, int L,
                                           int nk0, int K0, long long S, int M, int chunk, int n_chunks, float* partial,
-                                          float* bpartial, hipStream_t s, const WgRange* rng = nullptr);
+                                          float* bpartial, hipStream_t s, const WgRange* rng = nullptr, int dtype = 1);
 // t16: dz / feat in the split-recipe step kernel's T16 block layout (marf_wgrad.hip t16_off)
 hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* feat, int ldf, long long S, int M, int K,
                              int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s,
@@ -162,8 +162,8 @@ hipError_t marf_launch_wgrad(int dtype, const void* dz, int ldz, const void* fea
 struct WgFusedLayer {
     int kind;                 // 0: 256 x 256 LDS-DMA (hidden layer); 1: layer 0, feat_0 recomputed (256 x 96);
                               // 2: layer 0 stored (marf_launch_wgrad's kernel); 3: reduction only
-    const void* dz;           // kinds 0..2: [S][ldz] bf16
-    const void* feat;         // kinds 0, 2: [S][ldf] bf16
+    const void* dz;           // kinds 0..2: [S][ldz] bf16 (fp16x2: fp16)
+    const void* feat;         // kinds 0, 2: [S][ldf] bf16 (fp16x2: fp16)
     int ldz, ldf, M, K;
     float* partial;
     float* bpartial;
@@ -180,13 +180,14 @@ bool marf_wgrad_fused_ok(const WgFusedLayer* layers, int n_layers, long long S, 
                          long long Np_pad);
 hipError_t marf_launch_wgrad_fused(const WgFusedLayer* layers, int n_layers, long long S, int chunk, int n_chunks,
                                    const GeoDev& f0_geo, const float* c2f_w, int L, int nk0, const float* gscale,
-                                   const float* denom, hipStream_t s, hipStream_t s2, hipEvent_t fork, hipEvent_t join);
+                                   const float* denom, hipStream_t s, hipStream_t s2, hipEvent_t fork, hipEvent_t join,
+                                   int dtype = 1, float post = 1.f);  // dtype 2 / post 2^-10: the fp16x2 recipe
 hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* feat, long long S, int ldf, int K,
                                   int chunk, int n_chunks, float* partial, float* bpartial, hipStream_t s);
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
                                     int Ko, float* dW, float* db, hipStream_t s, const float* gscale = nullptr,
                                     const float* denom = nullptr, float* scratch = nullptr,
-                                    const int* kmap = nullptr);
+                                    const int* kmap = nullptr, float post = 1.f);
 hipError_t marf_launch_mlp_step(const marf::StepArgs& a, int dtype, int TP, int NW, size_t lds, int n_tiles, hipStream_t s);
 hipError_t marf_launch_c2f_weights(const marf::C2fDev& c, int L, float* out, hipStream_t s,
                                    const int* csrc = nullptr, int* cdst = nullptr, int cn = 0);

@@ -191,6 +191,8 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
 #define MARF_STEP2_J2 1
 #endif
     constexpr bool J2 = MARF_STEP2_J2 && NS == 2 && SPLIT && !SDZ && FIX;
+    // HF: the dgrad's gradient scale (the saved dz carry it; Step2NetPlan::gscale on the host)
+    constexpr float kGS = 1024.f;
     constexpr int R0Q = NKH / (FIX ? NK0F : NKH);  // layer-0 row tiles per stage (the host's r0)
     constexpr int R0F = R0Q < 1 ? 1 : (R0Q > NRT ? NRT : R0Q);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -460,8 +462,11 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
     typedef std::integral_constant<bool, false> PcOff;
     // one accumulation chain (a second, alternating accumulator measured no faster, and any change
     // of the summation order re-rolls the seed-3 basin: DESIGN.md §4)
-    auto mf = [&](f32x16& acc, const bf16x8& x, const bf16x8& y) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc, 0, 0, 0);
+    auto mf = [&](f32x16& acc, const uint4& x, const S2Frag& y) {
+        if constexpr (HF)  // (the fp16x2 recipe: every MFMA in fp16)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, x), y.h, acc, 0, 0, 0);
+        else
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, x), y.f, acc, 0, 0, 0);
     };
     // one 32-row output tile: acc (+)= A[ks] . B[ks] over NK k-steps from the slot
     //   MODE 0: plain; 1: split forward (hi.hi + hi.lo + lo.hi); 2: split dgrad (hi.B + lo.B)
@@ -477,10 +482,10 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
         constexpr int NK = decltype(nk_tag)::value;
         typedef std::integral_constant<int, 0> P0;
         typedef std::integral_constant<int, 1> P1;
-        const bf16x8* ah = reinterpret_cast<const bf16x8*>(slot + lane * 16);
-        const bf16x8* al = reinterpret_cast<const bf16x8*>(slot + C::LO + lane * 16);
+        const uint4* ah = reinterpret_cast<const uint4*>(slot + lane * 16);
+        const uint4* al = reinterpret_cast<const uint4*>(slot + C::LO + lane * 16);
         constexpr int P = NK < 4 ? NK : 4;
-        bf16x8 A0[4], A1[4];
+        uint4 A0[4], A1[4];
 #pragma unroll
         for (int u = 0; u < P; ++u) {
             A0[u] = ah[u * 64];
@@ -495,7 +500,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (MODE == 0) {
                 if (live) {
-                    mf(acc, A0[u], Bhi[ks].f);
+                    mf(acc, A0[u], Bhi[ks]);
                     hook(ksc, P0());
                     hook(ksc, P1());
                 }
@@ -503,30 +508,30 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                 if (live) piece();
             } else if constexpr (MODE == 2) {
                 if (live) {
-                    mf(acc, A0[u], Bhi[ks].f);
+                    mf(acc, A0[u], Bhi[ks]);
                     hook(ksc, P0());
                 }
                 if constexpr (refill) A0[u] = ah[(ks + P) * 64];
                 __builtin_amdgcn_sched_barrier(0);
                 if (live) {
-                    mf(acc, A1[u], Bhi[ks].f);
+                    mf(acc, A1[u], Bhi[ks]);
                     hook(ksc, P1());
                 }
                 if constexpr (refill) A1[u] = al[(ks + P) * 64];
                 if (live) piece();
             } else {
                 if (live) {
-                    mf(acc, A0[u], Bhi[ks].f);
+                    mf(acc, A0[u], Bhi[ks]);
                     hook(ksc, P0());
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (live) {
-                    mf(acc, A0[u], Blo[ks].f);
+                    mf(acc, A0[u], Blo[ks]);
                     hook(ksc, P1());
                 }
                 if constexpr (refill) A0[u] = ah[(ks + P) * 64];
                 __builtin_amdgcn_sched_barrier(0);
-                if (live) mf(acc, A1[u], Bhi[ks].f);
+                if (live) mf(acc, A1[u], Bhi[ks]);
                 if constexpr (refill) A1[u] = al[(ks + P) * 64];
                 if (live) piece();
             }
@@ -712,7 +717,10 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             : "v"(es.mw), "v"(pa[e]), "n"(bit));
         if constexpr (e & 1) {
             uint32_t w;
-            asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(es.vp), "v"(x));
+            if constexpr (HF)
+                asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(w) : "v"(es.vp), "v"(x));
+            else
+                asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(es.vp), "v"(x));
             es.hw[e >> 1] = w;
             if constexpr (SDZ) es.lw[e >> 1] = s2_pk(es.vp - s2_lo16(w), x - s2_hi16(w));
         } else {
@@ -728,7 +736,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             constexpr int b0 = 16 * 0 + 8 * (1 - (rt & 1)) + 7 - q, b1 = 16 * 1 + 8 * (1 - (rt & 1)) + 7 - q;
             const float x0 = __int_as_float(__builtin_amdgcn_sbfe((int)es.mw, b0, 1) & __float_as_int(pa[2 * q]));
             const float x1 = __int_as_float(__builtin_amdgcn_sbfe((int)es.mw, b1, 1) & __float_as_int(pa[2 * q + 1]));
-            es.hw[q] = s2_pk(x0, x1);
+            es.hw[q] = HF ? s2_pkh(x0, x1) : s2_pk(x0, x1);
             if constexpr (SDZ) es.lw[q] = s2_pk(x0 - s2_lo16(es.hw[q]), x1 - s2_hi16(es.hw[q]));
         });
     };
@@ -798,8 +806,9 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
     typedef std::integral_constant<bool, false> BF16t;
     // epilogue of a 32-row accumulator tile of set s, per pair q of registers (2q, 2q + 1): ReLU of
     // both (integer max with 0, as frelu), the fp16 operand pair into the next layer's fragment
-    // (k-step 2 rt + q / 4, word q mod 4), the bf16 pair for the saved tensor, its ReLU mask bits
-    // (from the bf16 pair, mask_pair's layout: the dgrad reads them as in the split recipe)
+    // (k-step 2 rt + q / 4, word q mod 4) -- also the saved tensor -- and the ReLU mask bits from the
+    // pair rounded to bf16 (mask_pair's layout; bf16 keeps fp32's exponent range, so a bit is set
+    // exactly for z > 0 as in the split recipe, where fp16 would drop 0 < z < 2^-25)
     struct Ep2 {
         float x[2][2];
         uint32_t bw[8];
@@ -890,9 +899,11 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             });
         }
     };
-    // finish of row tile rt of set s: the mask word (two row tiles per word) and the bf16 stores
+    // finish of row tile rt of set s: the mask word (two row tiles per word) and the stores of the
+    // saved tensor -- the fp16 operand fragments themselves (the weight gradients run in fp16)
     auto ffinish2 = [&](int l, auto rtc, auto sc, bool save, u16* srow, bool last) {
         constexpr int rt = decltype(rtc)::value, sset = decltype(sc)::value;
+        const S2Frag* O = sset ? Ol : Oh;
         Ep2& es = e2[sset];
         uint32_t* mks = mkl + sset * C::MSET;
         if constexpr ((rt & 1) == 0) {
@@ -901,12 +912,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
         } else {
             mks[(l * C::NMW + (rt >> 1)) * 64 + lane] = es.mpend | es.bits;
         }
-        if (save) {
-            S2Frag f0, f1;
-            f0.u = make_uint4(es.bw[0], es.bw[1], es.bw[2], es.bw[3]);
-            f1.u = make_uint4(es.bw[4], es.bw[5], es.bw[6], es.bw[7]);
-            store_rt(srow, rtc, f0, f1);
-        }
+        if (save) store_rt(srow, rtc, O[2 * rt], O[2 * rt + 1]);
     };
     f32x16 hacc[4];  // HF: current (0, 1) and previous (2, 3) row tile of sets 0, 1 (alternating)
 
@@ -965,7 +971,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                 Xs[sset][2] = X[2];
                 const float cd = h ? v : u;
                 // posenc + c2f: band groups of 4 (sin, cos) and the raw coordinate, as fp16 operands;
-                // feat_0 (bf16) only when the layer-0 weight gradient does not recompute it
+                // feat_0 (the fp16 operand) only when the layer-0 weight gradient does not recompute it
                 const bool st0 = !a.fwd_only && !a.feat0_recompute;
                 u16* row0 = st0 ? ly_ptr(0, 0) + (sl[sset] >> 5) * ly_int(0, 3) * 32 + pxl * 16 + 8 * h : nullptr;
                 s2_sfor<NK0F>([&](auto gc) {
@@ -991,7 +997,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                         f[0] = cd;
                     }
                     F0[sset][g].u = make_uint4(s2_pkh(f[0], f[1]), s2_pkh(f[2], f[3]), s2_pkh(f[4], f[5]), s2_pkh(f[6], f[7]));
-                    if (st0) s2_st16(row0 + 512 * g, make_uint4(s2_pk(f[0], f[1]), s2_pk(f[2], f[3]), s2_pk(f[4], f[5]), s2_pk(f[6], f[7])));
+                    if (st0) s2_st16(row0 + 512 * g, F0[sset][g].u);
                 });
                 if (st0) {
                     st_cur += NK0F;
@@ -1106,26 +1112,32 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             if (a.fwd_only) continue;  // render: the program holds the forward stages only
             s2_sfor<2>([&](auto sc) {
                 constexpr int sset = decltype(sc)::value;
-                // g operand of the last-layer dgrad (bf16, as the split recipe): lane half 0,
-                // k = [g hi (3), 0, g lo (3), 0]
+                // g operand of the last-layer dgrad: lane half 0, k = [g hi (3), 0, g lo (3), 0] as
+                // fp16 hi + lo of 2^10 g (GS: an exact power of two that lifts the dgrad's dz out of
+                // fp16's subnormal range; the dH partials and the weight gradients divide it out)
                 S2Frag Bg;
                 {
-                    float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                    uint32_t wv[4] = {0u, 0u, 0u, 0u};
                     if (h == 0) {
+                        u16 hi[3], lo[3];
 #pragma unroll
                         for (int c = 0; c < 3; ++c) {
-                            f[c] = gS[sset][c];
-                            f[4 + c] = gS[sset][c] - s2_lo16(s2_pk(gS[sset][c], 0.f));
+                            const float gs = gS[sset][c] * kGS;
+                            hi[c] = f2h(gs);
+                            lo[c] = f2h(gs - h2f(hi[c]));
                         }
+                        wv[0] = hi[0] | ((uint32_t)hi[1] << 16);
+                        wv[1] = hi[2];
+                        wv[2] = lo[0] | ((uint32_t)lo[1] << 16);
+                        wv[3] = lo[2];
                     }
-                    S2Frag dumm;
-                    s2_split8<false>(f, Bg, dumm);
+                    Bg.u = make_uint4(wv[0], wv[1], wv[2], wv[3]);
                 }
                 // last-layer weight gradient of the set's 32 pixels in fp16 (the operand the forward
                 // used): A = (2^10 g)^T as fp16 hi (rows 0-2) + lo (rows 4-6) -- an exact power of two
                 // that keeps |g| <= 0.5 in fp16's normal range -- B = feat^T through the LDS transpose
                 {
-                    constexpr float SC = 1024.f;
+                    constexpr float SC = kGS;
                     if (h == 0) {
 #pragma unroll
                         for (int c = 0; c < 3; ++c) {
@@ -1574,7 +1586,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                     c1 = (f32x16){};
                     if constexpr (rt == 0) {
                         S2T_BEGIN(9);
-                        gemm2(c0, c1, slot, Dh[0], Dh[1], NKHt(), nohook, PcOn(), BF16t());
+                        gemm2(c0, c1, slot, Dh[0], Dh[1], NKHt(), nohook, PcOn(), std::integral_constant<bool, HF>());
                         S2T_END(9);
                     } else {
                         typedef std::integral_constant<int, rt - 1> RP;
@@ -1587,7 +1599,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                                 constexpr int sset = ks >> 3;
                                 bstep(ebs[sset], sset ? q1 : q0, std::integral_constant<int, 2 * (ks & 7) + p>(), RP());
                             }
-                        }, PcOn(), BF16t());
+                        }, PcOn(), std::integral_constant<bool, HF>());
                         S2T_END(9);
                         S2T_BEGIN(11);
                         bfinish(ebs[0], Do[0], RP(), brow[0]);
@@ -1715,6 +1727,9 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             });
         }
         S2T_END(2);
+        if constexpr (HF) {  // (the fp16x2 dgrad carries 2^10 g: exact)
+            s2_sfor<NS>([&](auto sc) { dc[decltype(sc)::value] *= 1.0f / kGS; });
+        }
         S2T_BEGIN(3);
         // (u, v) = X[:2] / (X[2] + 1e-8) backward, then the bmm backward -> dH partial of the wave
         {
@@ -1953,7 +1968,7 @@ __global__ void k_pack2(const float* __restrict__ params, u16* __restrict__ prog
         }
         u16 out = 0;
         if (have) {
-            if (a.fwd_f16 && kind <= 1) {  // the fp16x2 recipe's forward stages: fp16 hi + lo
+            if (a.fwd_f16) {  // the fp16x2 recipe: every stage fp16 hi + lo
                 const u16 hi = f2h(val);
                 out = part == 0 ? hi : f2h(val - h2f(hi));
             } else {

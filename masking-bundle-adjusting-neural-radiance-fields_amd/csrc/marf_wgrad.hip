@@ -392,14 +392,14 @@ MARF_DEV void wgrad_dma_body(const WgArgs& a, int chunk_id, int ob, char* smem) 
         const int ng = a.f0.nk0 - 1;
         const int g = k0 >> 2, j = k0 & 3;
         if (g < ng) {
-            *reinterpret_cast<uint32_t*>(row + 2 * (16 * g + 8 * h + j)) = PrecBF16::pk2(sn[0], sn[1]);
-            *reinterpret_cast<uint32_t*>(row + 2 * (16 * g + 8 * h + 4 + j)) = PrecBF16::pk2(cs[0], cs[1]);
+            *reinterpret_cast<uint32_t*>(row + 2 * (16 * g + 8 * h + j)) = P::pk2(sn[0], sn[1]);
+            *reinterpret_cast<uint32_t*>(row + 2 * (16 * g + 8 * h + 4 + j)) = P::pk2(cs[0], cs[1]);
         }
         // columns 16 ng .. 95: the raw coordinates (16 ng + 8 h) and zeros, one pair per thread
         for (int c = 16 * ng + 2 * sub; c < KF; c += 32) {
             const int hc = (c - 16 * ng) >> 3;
             const float val = (c - 16 * ng) == 8 * hc && hc < 2 ? (hc ? v : u) : 0.f;
-            *reinterpret_cast<uint32_t*>(row + 2 * c) = PrecBF16::pk2(val, 0.f);
+            *reinterpret_cast<uint32_t*>(row + 2 * c) = P::pk2(val, 0.f);
         }
       }
     };
@@ -685,6 +685,7 @@ struct WgRedJob {
     float* dW;
     float* db;
     const int* kmap;
+    float post;  // exact power of two the partials carry the inverse of (1, or the fp16x2 recipe's 2^-10)
 };
 struct WgRedArgs {
     WgRedJob job[WF_MAXJ];
@@ -697,7 +698,7 @@ struct WgRedArgs {
 MARF_DEV void wgrad_reduce_block(const float* __restrict__ partial, const float* __restrict__ bpartial, int n_chunks,
                                  int M, int K, int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db,
                                  const float* __restrict__ gscale, const float* __restrict__ denom,
-                                 const int* __restrict__ kmap, int blk, float (*red)[64]) {
+                                 const int* __restrict__ kmap, int blk, float (*red)[64], float post = 1.f) {
     const long long n = (long long)Mo * Ko;
     const long long e = blk * 64LL + (threadIdx.x & 63);
     const int g = threadIdx.x >> 6;
@@ -730,6 +731,7 @@ MARF_DEV void wgrad_reduce_block(const float* __restrict__ partial, const float*
         float t = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
         // fused step: the partials carry the unit-upstream gradient without 1/denominator
         if (gscale) t = t * (gscale[0] / denom[0]);
+        if (post != 1.f) t = t * post;  // (exact: a power of two)
         if (e < n) dW[e] = t;
         else db[e - n] = t;
     }
@@ -741,7 +743,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce_layers(WgRedArgs r) {
     while (j < r.n_jobs - 1 && (int)blockIdx.x >= r.job[j + 1].blk0) ++j;
     const WgRedJob& q = r.job[j];
     wgrad_reduce_block(q.partial, q.bpartial, q.n_chunks, q.M, q.K, q.Mo, q.Ko, q.dW, q.db, r.gscale, r.denom, q.kmap,
-                       (int)blockIdx.x - q.blk0, red);
+                       (int)blockIdx.x - q.blk0, red, q.post);
 }
 
 // Fixed-order sum of the chunk partials into the flat fp32 gradient (nn.Linear layout [M][K],
@@ -752,9 +754,9 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
                                                       const float* __restrict__ bpartial, int n_chunks, int M, int K,
                                                       int Mo, int Ko, float* __restrict__ dW, float* __restrict__ db,
                                                       const float* __restrict__ gscale, const float* __restrict__ denom,
-                                                      const int* __restrict__ kmap) {
+                                                      const int* __restrict__ kmap, float post) {
     __shared__ float red[4][64];
-    wgrad_reduce_block(partial, bpartial, n_chunks, M, K, Mo, Ko, dW, db, gscale, denom, kmap, blockIdx.x, red);
+    wgrad_reduce_block(partial, bpartial, n_chunks, M, K, Mo, Ko, dW, db, gscale, denom, kmap, blockIdx.x, red, post);
 }
 
 }  // namespace marf
@@ -879,7 +881,7 @@ bool marf_wgrad_l0_recompute_ok(int M, int ldz, int ldf0, long long S, int chunk
 
 hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev& geo, const float* c2f_w, int L,
                                           int nk0, int K0, long long S, int M, int chunk, int n_chunks, float* partial,
-                                          float* bpartial, hipStream_t s, const WgRange* rng) {
+                                          float* bpartial, hipStream_t s, const WgRange* rng, int dtype) {
     WgArgs a;
     memset(&a, 0, sizeof(a));
     if (rng) {
@@ -903,6 +905,8 @@ hipError_t marf_launch_wgrad_l0_recompute(const void* dz, int ldz, const GeoDev&
     a.chunk = chunk;
     a.partial = partial;
     a.bpartial = bpartial;
+    // (dtype 2: the fp16x2 recipe's dz_1 and feat_0 in fp16)
+    if (dtype == 2) return launch_wg_dma<PrecF16, 96, true, true>(a, n_chunks, s);
     return launch_wg_dma<PrecBF16, 96, true, true>(a, n_chunks, s);
 }
 
@@ -942,7 +946,7 @@ bool marf_wgrad_fused_ok(const WgFusedLayer* layers, int n_layers, long long S, 
 hipError_t marf_launch_wgrad_fused(const WgFusedLayer* layers, int n_layers, long long S, int chunk, int n_chunks,
                                    const GeoDev& f0_geo, const float* c2f_w, int L, int nk0, const float* gscale,
                                    const float* denom, hipStream_t s, hipStream_t s2, hipEvent_t fork,
-                                   hipEvent_t join) {
+                                   hipEvent_t join, int dtype, float post) {
     hipError_t e;
     // layer 0 on s2, beside the hidden layers
     const WgFusedLayer* l0 = nullptr;
@@ -952,9 +956,9 @@ hipError_t marf_launch_wgrad_fused(const WgFusedLayer* layers, int n_layers, lon
         if ((e = hipEventRecord(fork, s)) != hipSuccess || (e = hipStreamWaitEvent(s2, fork, 0)) != hipSuccess) return e;
         if (l0->kind == 1)
             e = marf_launch_wgrad_l0_recompute(l0->dz, l0->ldz, f0_geo, c2f_w, L, nk0, l0->K, S, l0->M, chunk, n_chunks, l0->partial,
-                                               l0->bpartial, s2);
+                                               l0->bpartial, s2, nullptr, dtype);
         else
-            e = marf_launch_wgrad(1, l0->dz, l0->ldz, l0->feat, l0->ldf, S, l0->M, l0->K, chunk, n_chunks, l0->partial,
+            e = marf_launch_wgrad(dtype, l0->dz, l0->ldz, l0->feat, l0->ldf, S, l0->M, l0->K, chunk, n_chunks, l0->partial,
                                   l0->bpartial, s2, nullptr, true);
         if (e != hipSuccess) return e;
         if ((e = hipEventRecord(join, s2)) != hipSuccess) return e;
@@ -984,11 +988,15 @@ hipError_t marf_launch_wgrad_fused(const WgFusedLayer* layers, int n_layers, lon
     }
     if (nh) {
         const size_t lds = (size_t)WG_NBUF_H * WG_SPH * (512 + 256 * 2);
-        typedef PrecBF16 P;
-        e = ensure_dynamic_lds((const void*)k_wgrad_dma_layers<P, WG_NBUF_H, WG_SPH, 256>, lds);
+        auto go = [&](auto prec) -> hipError_t {
+            typedef decltype(prec) P;
+            hipError_t er = ensure_dynamic_lds((const void*)k_wgrad_dma_layers<P, WG_NBUF_H, WG_SPH, 256>, lds);
+            if (er != hipSuccess) return er;
+            hipLaunchKernelGGL((k_wgrad_dma_layers<P, WG_NBUF_H, WG_SPH, 256>), dim3(nh * n_chunks), dim3(512), lds, s, la);
+            return hipGetLastError();
+        };
+        e = dtype == 2 ? go(PrecF16()) : go(PrecBF16());  // (fp16x2: fp16 saved tensors)
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_wgrad_dma_layers<P, WG_NBUF_H, WG_SPH, 256>), dim3(nh * n_chunks), dim3(512), lds, s, la);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (l0 && (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess) return e;
     // every layer's reduction: one launch, in the layers' order
@@ -1011,6 +1019,7 @@ hipError_t marf_launch_wgrad_fused(const WgFusedLayer* layers, int n_layers, lon
         q.dW = Ly.dW;
         q.db = Ly.db;
         q.kmap = Ly.kmap;
+        q.post = Ly.kind == 3 ? 1.f : post;  // (the last layer's partials: unscaled in the step kernel)
         q.blk0 = blk;
         blk += (int)(((long long)Ly.Mo * Ly.Ko + Ly.Mo + 63) / 64);
     }
@@ -1034,7 +1043,7 @@ hipError_t marf_launch_wgrad_last(int dtype, const float* glast, const void* fea
 
 hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial, int n_chunks, int M, int K, int Mo,
                                     int Ko, float* dW, float* db, hipStream_t s, const float* gscale,
-                                    const float* denom, float* scratch, const int* kmap) {
+                                    const float* denom, float* scratch, const int* kmap, float post) {
     if (n_chunks > 1024 && scratch) {
         // fold into G <= 256 groups first (n_chunks up to millions of partials)
         const int per = (n_chunks + 255) / 256;
@@ -1053,6 +1062,6 @@ hipError_t marf_launch_wgrad_reduce(const float* partial, const float* bpartial,
     long long n = (long long)Mo * Ko + Mo;
     int blocks = (int)((n + 63) / 64);
     hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, s, partial, bpartial, n_chunks, M, K, Mo, Ko, dW, db,
-                       gscale, denom, kmap);
+                       gscale, denom, kmap, post);
     return hipGetLastError();
 }

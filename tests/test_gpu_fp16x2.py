@@ -1,7 +1,7 @@
 """The fp16x2 recipe (include/marf.h MARF_FP16X2, opt.precision "fp16x2"): k_step2h, the fused step
-with an fp16 forward -- weights fp16 hi + lo, activations single fp16, W_hi a + W_lo a (2 MFMAs per
-MAC) -- over TWO pixel sets per pass of the forward weight stages, and the split recipe's bf16
-dgrad, saved tensors and weight gradients.
+with every MFMA in fp16 -- weights fp16 hi + lo, activations and dz single fp16 (2 MFMAs per MAC in
+the forward and the dgrad), dz carrying an exact 2^10 gradient scale -- over TWO pixel sets per pass
+of every weight stage; fp16 saved tensors and fp16 weight gradients.
 
 Bounds (north_star bf16: rgb within 1e-2, gradients within 1e-2), against oracle.PlanarStep (rgb,
 loss) and the reference's ops in float64 (gradients, tests/test_gpu_parity.py _compare_step):
@@ -10,8 +10,8 @@ loss) and the reference's ops in float64 (gradients, tests/test_gpu_parity.py _c
   * d warp cosine >= 0.999 and error <= max(1e-2, 10 x the reference's own fp32 error): d warp is
     a sum over 10^5 pixels that cancels, and the fp16 forward's rgb error is smooth over the image
     (correlated, not averaged out), so its share of the cancelled sum is larger than the split-bf16
-    recipe's -- measured 2.4e-2 at c3x2 (4.6x the reference's fp32 error; bf16x3 1.5x), the same in
-    an emulation of the recipe in the fp32 kernels (tools/emu_grad_err.py).
+    recipe's (measured in an emulation of the recipes in the fp32 kernels, tools/emu_grad_err.py,
+    DESIGN.md §4).
 Structure: reruns bit-identical, d loss x 2 -> every gradient x 2 exactly, per-pixel results
 independent of how a block pairs its tiles (the second set of a block's last group may be missing).
 """
@@ -114,7 +114,7 @@ def test_fp16x2_headline_step():
     reruns bit-identical, d loss x 2 -> every gradient x 2 exactly, rgb of 512 sampled pixels of
     every patch within 1e-2 of the oracle's fp32 forward, d warp of two patches within 1e-2 of the
     float64 reference ops with cosine >= 0.999, and the step's gradients against the bf16x3 recipe's
-    (the same dgrad arithmetic on a different forward) at cosine >= 0.999."""
+    on the same state at cosine >= 0.999."""
     import cpu_ref
     import step_bits
     m, var = step_bits.build_case("c3x64", precision="fp16x2")
