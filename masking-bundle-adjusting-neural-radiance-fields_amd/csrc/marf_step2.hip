@@ -933,6 +933,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
         if constexpr (HF) {
             // ---- the fp16x2 forward of the group's two pixel sets (set 1 of a last, single tile
             //      repeats set 0's inputs; its stores go to the sink rows, its loss terms are zero)
+            S2T_BEGIN(4);
             const int gp = (it / NS) & 1;
             int tl[2];
             long long sl[2];  // the set's first pixel slot of the wave (a missing set: the sink rows)
@@ -1007,6 +1008,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                     }
                 }
             });
+            S2T_END(4);
             // ---- forward, layer 0 then the hidden layers: one stage per 32-row output tile (layer
             //      0: r0 row tiles per stage); the epilogue of row tile rt-1 of both sets runs in the
             //      MFMA gaps of row tile rt, the last row tile's right after its own MFMAs
@@ -1027,8 +1029,10 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                     f32x16& q0 = hacc[(rt & 1) ? 0 : 2];
                     f32x16& q1 = hacc[(rt & 1) ? 1 : 3];
                     const int sub = l == 0 ? rt % R0F : 0;
+                    S2T_BEGIN(15);
                     c0 = bias_init(boff, rt);  // (before the stage wait: the reads overlap it)
                     c1 = c0;
+                    S2T_END(15);
                     if (sub == 0) slotb = stage_begin(l == 0);  // layer 0: the pieces in a burst
                     const char* slot = slotb + sub * NK * 1024;
                     if (l == 0 && rt == 0 && it + NS < my_tiles) {
@@ -1036,24 +1040,34 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                         st_cur += 2;
                     }
                     if constexpr (rt == 0) {
+                        S2T_BEGIN(8);
                         gemm2(c0, c1, slot, B0, B1, nk_tag, nohook, PcL(), F16t());
+                        S2T_END(8);
                     } else {
                         typedef std::integral_constant<int, rt - 1> RP;
                         e2[0].bits = 0;
                         e2[1].bits = 0;
+                        S2T_BEGIN(8);
                         gemm2(c0, c1, slot, B0, B1, nk_tag, [&](auto ksc, auto pc) {
                             hook2(q0, q1, Oh, Ol, RP(), ksc, pc, ppk_tag);
                         }, PcL(), F16t());
+                        S2T_END(8);
+                        S2T_BEGIN(13);
                         free_pairs(q0, q1, Oh, Ol, RP(), std::integral_constant<int, PPK * NK>());
+                        S2T_END(13);
+                        S2T_BEGIN(10);
                         ffinish2(l, RP(), I0(), save, srow[0], false);
                         ffinish2(l, RP(), I1(), save, srow[1], false);
+                        S2T_END(10);
                     }
                     if constexpr (rt == NRT - 1) {
+                        S2T_BEGIN(13);
                         e2[0].bits = 0;
                         e2[1].bits = 0;
                         free_pairs(c0, c1, Oh, Ol, rtc, I0());
                         ffinish2(l, rtc, I0(), save, srow[0], true);
                         ffinish2(l, rtc, I1(), save, srow[1], true);
+                        S2T_END(13);
                     }
                 });
 #pragma unroll
@@ -1062,8 +1076,13 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                     Bl[k] = Ol[k];
                 }
             };
+            S2T_BEGIN(5);
+            S2T_BEGIN(14);
             fwd2_layer(0, F0[0], F0[1], std::integral_constant<int, NK0F>(), I2());
+            S2T_END(14);
             for (int l = 1; l < nl - 1; ++l) fwd2_layer(l, Bh, Bl, NKHt(), I1());
+            S2T_END(5);
+            S2T_BEGIN(6);
 
             // ---- last layer of both sets: 3 outputs (rows 0..2 of one tile), sigmoid, masked MSE, d rgb
             float gS[2][3];
@@ -1109,7 +1128,10 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                     st_cur += 1;
                 });
             }
-            if (a.fwd_only) continue;  // render: the program holds the forward stages only
+            if (a.fwd_only) {  // render: the program holds the forward stages only
+                S2T_END(6);
+                continue;
+            }
             s2_sfor<2>([&](auto sc) {
                 constexpr int sset = decltype(sc)::value;
                 // g operand of the last-layer dgrad: lane half 0, k = [g hi (3), 0, g lo (3), 0] as
@@ -1178,6 +1200,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
                 cs.tile = real[sset] ? tl[sset] : -1;
                 ss[sset] = cs;
             });
+            S2T_END(6);
         } else {
         for (int si = 0; si < nset; ++si) {
             S2T_BEGIN(4);
