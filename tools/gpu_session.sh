@@ -13,6 +13,8 @@
 #   cfg                       secondary bench lines (tools/bench_configs.sh)
 #   pmc=<config>/<precision>  FETCH_SIZE / WRITE_SIZE / matrix-core passes (tools/pmc_traffic.sh)
 #   basin=<draws>:<n>=<recipe>;...  seed-3 C1 basin rates over one-ulp init draws (tools/basin_table.py)
+#   phases                    step-kernel phase stamps, bf16x3 and fp16x2 (lib/libmarf_stamps.so)
+#   c1graph                   C1 eager vs captured iteration, bf16x3 and fp16x2, alternating twice
 # Every GPU step has its own time limit; the session stops at the first failure, abort or timeout.
 set -o pipefail
 TAG=$1; shift
@@ -94,6 +96,24 @@ for step in "$@"; do
         --chunk ${BASIN_CHUNK:-5} --deadline ${BASIN_DEADLINE:-800} --hard-deadline ${BASIN_HARD:-1000} --out $OUT/basin "${RS[@]}" > $OUT/basin.log 2>&1
       RC=$?; tail -6 $OUT/basin.log
       [ $RC = 0 ] || { echo "basin exit $RC: stopping"; exit $RC; } ;;
+    phases)
+      # in-kernel phase stamps of the step kernel per recipe (lib/libmarf_stamps.so: build_lib.py --stamps)
+      for P in bf16x3 fp16x2; do
+        MARF_LIB=$LIBD/libmarf_stamps.so timeout -k 10 200 python -u tools/step2_phases.py --precision $P > $OUT/phases_$P.log 2>&1 \
+          || { echo "phases $P failed"; tail -5 $OUT/phases_$P.log; exit 1; }
+        grep "tile loop total" $OUT/phases_$P.log
+      done ;;
+    c1graph)
+      # C1 per recipe, eager against the captured iteration (--graph), alternating twice
+      for rep in 1 2; do
+        for A in "bf16x3" "bf16x3 --graph" "fp16x2" "fp16x2 --graph"; do
+          read -ra AA <<< "$A"
+          N=c1_${AA[0]}${AA[1]:+_graph}_$rep
+          timeout -k 10 200 python bench.py --config c1 --precision ${AA[0]} ${AA[1]} --steps 50 --warmup 5 --no-cpu-baseline --no-render \
+            > $OUT/$N.json 2> $OUT/$N.err || { echo "c1 $A failed"; tail -5 $OUT/$N.err; exit 1; }
+          line $OUT/$N.json "$N"
+        done
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
