@@ -46,8 +46,9 @@ static inline long long rup(long long x, long long m) { return (x + m - 1) / m *
 // step2 plan (the pixel-per-wave fused step, marf_step2.hip), filled by plan_step2_net
 struct Step2NetPlan {
     int variant;           // -1: not available for this net; 0: bf16 (8 waves); 1: split bf16 (4 waves);
-                           // 2: bf16 on 4 waves (diagnostic); 3: fp16x2 (fp16 forward of two pixel sets
-                           // per stage, split-bf16 dgrad; 4 waves, compile-time layer 0 only)
+                           // 2: bf16 on 4 waves (diagnostic); 3: fp16x2 (split-fp16 weights, fp16
+                           // activations and dz, two pixel sets per forward and dgrad stage; 4 waves,
+                           // compile-time layer 0 only)
     bool dz;               // variant 1 with the dgrad's dz split too (MARF_STEP2_DZ=1 at net creation)
     int NW, NS, HM, MAXR, NMW, slot, nk0, nta, n_stages, nbias, Kl, ldf0;
     int PX, TPX;           // pixels per wave, pixel slots per block tile

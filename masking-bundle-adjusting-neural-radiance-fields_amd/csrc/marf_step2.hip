@@ -171,12 +171,14 @@ struct S2Cfg {
 // W_hi^T dz_hi + W_lo^T dz_hi + W_hi^T dz_lo (the forward's three terms), one pixel set per dgrad
 // pass; dz_1 (the layer-0 adjoint's operand) and the saved dz stay bf16 hi.  DESIGN.md §4: the
 // recipe whose emulation reaches fp32's basin rate.
-// HF (the fp16x2 recipe, MARF_FP16X2): the forward in fp16 -- weights fp16 hi + lo, activations
-// single fp16, W_hi a + W_lo a (2 MFMAs per MAC instead of 3) -- and, since one 32-pixel set's
-// operands then take half the registers, the forward of a group's TWO tiles in one pass over the
-// forward stages (every weight fragment read from LDS once for both sets, every stage DMA'd once per
-// pair of tiles, as the dgrad already is).  The dgrad, the saved tensors (bf16) and the weight
-// gradients are the split recipe's.  Compile-time layer-0 instantiations only (full-width nets).
+// HF (the fp16x2 recipe, MARF_FP16X2): every MFMA in fp16 -- weights fp16 hi + lo, activations and
+// dz single fp16, W_hi a + W_lo a in the forward and W_hi^T dz + W_lo^T dz in the dgrad (2 MFMAs per
+// MAC) -- and, since one 32-pixel set's operands then take half the registers, the forward of a
+// group's TWO tiles in one pass over the forward stages (every weight fragment read from LDS once
+// for both sets, every stage DMA'd once per pair of tiles, as the dgrad already is).  dz carries an
+// exact 2^10 gradient scale; the saved tensors are fp16 and the weight gradients run in fp16
+// (marf_wgrad.hip PrecF16, the 2^-10 in the reduction).  Compile-time layer-0 instantiations only
+// (full-width nets).
 template <int HM, bool SPLIT, int NW, int MAXR, int NK0F, int NTAF, bool DZ, bool HF = false>
 __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Args& a) {
     typedef S2Cfg<HM, SPLIT, NW, MAXR, DZ> C;
@@ -191,7 +193,8 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
 #define MARF_STEP2_J2 1
 #endif
     constexpr bool J2 = MARF_STEP2_J2 && NS == 2 && SPLIT && !SDZ && FIX;
-    // HF: the dgrad's gradient scale (the saved dz carry it; Step2NetPlan::gscale on the host)
+    // HF: the dgrad's gradient scale (the saved dz carry it; the host's weight-gradient reduction
+    // multiplies by its inverse, marf_abi.hip step2_backward)
     constexpr float kGS = 1024.f;
     constexpr int R0Q = NKH / (FIX ? NK0F : NKH);  // layer-0 row tiles per stage (the host's r0)
     constexpr int R0F = R0Q < 1 ? 1 : (R0Q > NRT ? NRT : R0Q);
@@ -1876,7 +1879,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2dz(Step2Args a) {
     k_step2_body<HM, SPLIT, NW, MAXR, NK0F, NTAF, true>(a);
 }
 
-// the fp16x2 recipe (MARF_FP16X2): fp16 forward of two pixel sets per stage, the split dgrad
+// the fp16x2 recipe (MARF_FP16X2): split-fp16 weights, fp16 forward and dgrad of two pixel sets per stage
 template <int HM, int NW, int MAXR, int NK0F, int NTAF>
 __global__ __launch_bounds__(NW * 64, NW / 4) void k_step2h(Step2Args a) {
     k_step2_body<HM, true, NW, MAXR, NK0F, NTAF, false, true>(a);

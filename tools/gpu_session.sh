@@ -50,7 +50,7 @@ for step in "$@"; do
       line $OUT/bench.json bench ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
-         python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render > $OUT/prof.log 2>&1) || { echo "rocprof failed"; tail -5 $OUT/prof.log; exit 1; }
+         python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render --no-alt-recipe > $OUT/prof.log 2>&1) || { echo "rocprof failed"; tail -5 $OUT/prof.log; exit 1; }
       find $OUT/prof -name "*kernel_stats*" | head -3 ;;
     bits)
       timeout -k 10 300 python tools/make_step2_bits.py $OUT/step2_bits.json > $OUT/bits.log 2>&1 || { echo "bits failed"; tail -5 $OUT/bits.log; exit 1; }
@@ -60,7 +60,7 @@ for step in "$@"; do
       for rep in 1 2; do
         for v in "${VS[@]}"; do
           if [ "$v" = default ]; then L=""; TO=""; else L=$LIBD/libmarf_$v.so; TO=$([[ $v == ab_* ]] && echo 1); fi
-          MARF_LIB=$L MARF_AB_TIMING_ONLY=$TO timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render \
+          MARF_LIB=$L MARF_AB_TIMING_ONLY=$TO timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render --no-alt-recipe \
             > $OUT/ab_$v.json 2> $OUT/ab_$v.err || { echo "ab $v failed"; tail -5 $OUT/ab_$v.err; exit 1; }
           line $OUT/ab_$v.json "$v"
         done
@@ -75,7 +75,7 @@ for step in "$@"; do
         for v in "${VS[@]}"; do
           for c in "${CS[@]}"; do
             if [ $c = c1 ]; then A=(--config c1 --precision bf16x3 --steps 30 --warmup 3); else A=(--config $c --steps 10 --warmup 2); fi
-            env $VAR=$v timeout -k 10 200 python bench.py "${A[@]}" --no-cpu-baseline --no-render \
+            env $VAR=$v timeout -k 10 200 python bench.py "${A[@]}" --no-cpu-baseline --no-render --no-alt-recipe \
               > $OUT/envab_${c}_$v.json 2> $OUT/envab_${c}_$v.err || { echo "envab $c $v failed"; tail -5 $OUT/envab_${c}_$v.err; exit 1; }
             line $OUT/envab_${c}_$v.json "$c $VAR=$v"
           done
@@ -85,7 +85,7 @@ for step in "$@"; do
       bash tools/bench_configs.sh $TAG/cfg || exit 1 ;;
     pmc=*)
       C=${step#pmc=}
-      bash tools/pmc_traffic.sh $TAG/pmc_${C%/*} ${C%/*} ${C#*/} || exit 1 ;;
+      bash tools/pmc_traffic.sh $TAG/pmc_${C%/*}_${C#*/} ${C%/*} ${C#*/} || exit 1 ;;
     basin=*)
       # basin=<draws>:<name>=<recipe>[;<name>=<recipe>...]  the seed-3 C1 3000-step run over one-ulp
       # init draws per recipe (tools/basin_table.py; a recipe = precision[:VAR=value,...]) ->
@@ -109,7 +109,7 @@ for step in "$@"; do
         for A in "bf16x3" "bf16x3 --graph" "fp16x2" "fp16x2 --graph"; do
           read -ra AA <<< "$A"
           N=c1_${AA[0]}${AA[1]:+_graph}_$rep
-          timeout -k 10 200 python bench.py --config c1 --precision ${AA[0]} ${AA[1]} --steps 50 --warmup 5 --no-cpu-baseline --no-render \
+          timeout -k 10 200 python bench.py --config c1 --precision ${AA[0]} ${AA[1]} --steps 50 --warmup 5 --no-cpu-baseline --no-render --no-alt-recipe \
             > $OUT/$N.json 2> $OUT/$N.err || { echo "c1 $A failed"; tail -5 $OUT/$N.err; exit 1; }
           line $OUT/$N.json "$N"
         done

@@ -17,7 +17,7 @@ for CTR in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_
   i=$((i+1))
   (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $CTR --kernel-trace --output-format csv -d $OUT/pass$i -o run \
      --kernel-include-regex "k_mlp|k_wgrad|k_step2|k_step3|k_prologue" -- python3 $ROOT/bench.py --config $CFG --precision $PREC \
-     --steps 2 --warmup 1 --no-cpu-baseline --no-render "$@" > $OUT/pass$i.log 2>&1) || { echo "pass $i ($CTR) failed"; tail -5 $OUT/pass$i.log; exit 1; }
+     --steps 2 --warmup 1 --no-cpu-baseline --no-render --no-alt-recipe "$@" > $OUT/pass$i.log 2>&1) || { echo "pass $i ($CTR) failed"; tail -5 $OUT/pass$i.log; exit 1; }
 done
 # (profiles/ does not come back from a GPU box: the updated json lands in $OUT, copied back by hand)
 cp profiles/pmc_traffic.json $OUT/pmc_traffic.json 2>/dev/null
