@@ -7,8 +7,9 @@
 #   bench                     the default bench line (C3 headline, CPU baseline) -> <tag>/bench.json
 #   prof                      rocprofv3 --kernel-trace --stats of a short C3 bench -> <tag>/prof/
 #   bits                      tools/make_step2_bits.py -> <tag>/step2_bits.json
-#   ab=<v1,v2,...>            C3 bench of lib/libmarf_<v>.so variants ("default" = lib/libmarf.so),
-#                             alternating twice (timing-only variants: MARF_AB_TIMING_ONLY=1)
+#   ab=<v1,v2,...>[@prec]     C3 bench of lib/libmarf_<v>.so variants ("default" = lib/libmarf.so),
+#                             alternating twice, in recipe prec (default bf16x3; timing-only variants
+#                             ab_*: MARF_AB_TIMING_ONLY=1)
 #   envab=VAR:v1,v2[:c1,c3]   C1 / C3 benches with VAR=v1, v2, ... alternating twice (library A/B switches)
 #   cfg                       secondary bench lines (tools/bench_configs.sh)
 #   pmc=<config>/<precision>  FETCH_SIZE / WRITE_SIZE / matrix-core passes (tools/pmc_traffic.sh)
@@ -56,13 +57,16 @@ for step in "$@"; do
       timeout -k 10 300 python tools/make_step2_bits.py $OUT/step2_bits.json > $OUT/bits.log 2>&1 || { echo "bits failed"; tail -5 $OUT/bits.log; exit 1; }
       tail -2 $OUT/bits.log ;;
     ab=*)
-      IFS=, read -ra VS <<< "${step#ab=}"
+      # ab=<v1,v2,...>[@<precision>]  (e.g. ab=default,prev@fp16x2: lib/libmarf_prev.so against the default)
+      SPEC=${step#ab=}; PR=bf16x3
+      if [[ $SPEC == *@* ]]; then PR=${SPEC#*@}; SPEC=${SPEC%@*}; fi
+      IFS=, read -ra VS <<< "$SPEC"
       for rep in 1 2; do
         for v in "${VS[@]}"; do
           if [ "$v" = default ]; then L=""; TO=""; else L=$LIBD/libmarf_$v.so; TO=$([[ $v == ab_* ]] && echo 1); fi
-          MARF_LIB=$L MARF_AB_TIMING_ONLY=$TO timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-render --no-alt-recipe \
-            > $OUT/ab_$v.json 2> $OUT/ab_$v.err || { echo "ab $v failed"; tail -5 $OUT/ab_$v.err; exit 1; }
-          line $OUT/ab_$v.json "$v"
+          MARF_LIB=$L MARF_AB_TIMING_ONLY=$TO timeout -k 10 200 python bench.py --precision $PR --steps 10 --warmup 2 --no-cpu-baseline --no-render --no-alt-recipe \
+            > $OUT/ab_${v}_${PR}_$rep.json 2> $OUT/ab_$v.err || { echo "ab $v failed"; tail -5 $OUT/ab_$v.err; exit 1; }
+          line $OUT/ab_${v}_${PR}_$rep.json "$v $PR"
         done
       done ;;
     envab=*)
