@@ -813,7 +813,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
     // pair rounded to bf16 (mask_pair's layout; bf16 keeps fp32's exponent range, so a bit is set
     // exactly for z > 0 as in the split recipe, where fp16 would drop 0 < z < 2^-25)
     struct Ep2 {
-        float x[2][2];
+        float x[4][2];
         uint32_t bw[8];
         uint32_t bits, mpend;
     };
@@ -866,6 +866,11 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
         typedef std::integral_constant<int, PPK * ks + 1> Pb;
         if constexpr (PPK == 1) {
             hop(p0s, p1s, O0, O1, rtc, Pa(), I0(), pc);
+        } else if constexpr (PPK == 4) {
+            // (layer 0's 5-k-step GEMMs: all 16 pairs in the gaps) gap p: op p of pairs 4 ks .. 4 ks + 3
+            s2_sfor<4>([&](auto jc) {
+                hop(p0s, p1s, O0, O1, rtc, std::integral_constant<int, PPK * ks + decltype(jc)::value>(), jc, pc);
+            });
         } else {
             static_assert(PPK == 2, "pairs per k-step");
             if constexpr (p == 0) {
@@ -1081,7 +1086,7 @@ __device__ __attribute__((always_inline)) inline void k_step2_body(const Step2Ar
             };
             S2T_BEGIN(5);
             S2T_BEGIN(14);
-            fwd2_layer(0, F0[0], F0[1], std::integral_constant<int, NK0F>(), I2());
+            fwd2_layer(0, F0[0], F0[1], std::integral_constant<int, NK0F>(), std::integral_constant<int, 4>());
             S2T_END(14);
             for (int l = 1; l < nl - 1; ++l) fwd2_layer(l, Bh, Bl, NKHt(), I1());
             S2T_END(5);

@@ -16,6 +16,7 @@
 #   basin=<draws>:<n>=<recipe>;...  seed-3 C1 basin rates over one-ulp init draws (tools/basin_table.py)
 #   phases                    step-kernel phase stamps, bf16x3 and fp16x2 (lib/libmarf_stamps.so)
 #   c1graph                   C1 eager vs captured iteration, bf16x3 and fp16x2, alternating twice
+#   rbits=<v1,v2>[@prec]      a recipe's step bit images per library (tools/recipe_bits.py), compared
 # Every GPU step has its own time limit; the session stops at the first failure, abort or timeout.
 set -o pipefail
 TAG=$1; shift
@@ -118,6 +119,25 @@ for step in "$@"; do
           line $OUT/$N.json "$N"
         done
       done ;;
+    rbits=*)
+      # rbits=<v1,v2,...>[@precision]: bit images of a recipe's step per library (tools/recipe_bits.py),
+      # compared: identical = the change is bit-neutral for that recipe
+      SPEC=${step#rbits=}; PR=fp16x2
+      if [[ $SPEC == *@* ]]; then PR=${SPEC#*@}; SPEC=${SPEC%@*}; fi
+      IFS=, read -ra VS <<< "$SPEC"
+      for v in "${VS[@]}"; do
+        if [ "$v" = default ]; then L=""; else L=$LIBD/libmarf_$v.so; fi
+        MARF_LIB=$L timeout -k 10 300 python tools/recipe_bits.py --precision $PR $OUT/rbits_${v}_$PR.json > $OUT/rbits_$v.log 2>&1 \
+          || { echo "rbits $v failed"; tail -5 $OUT/rbits_$v.log; exit 1; }
+      done
+      python - $OUT/rbits_*_$PR.json <<'PY'
+import json, sys
+r = [json.load(open(f)) for f in sys.argv[1:]]
+for c in r[0]["cases"]:
+    same = all(x["cases"][c]["bits"] == r[0]["cases"][c]["bits"] for x in r)
+    print(f"{c:10s} {r[0]['cases'][c]['kernel']:10s} {'identical' if same else 'DIFFER'}")
+PY
+      ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
