@@ -7,7 +7,8 @@ Bounds (north_star bf16: rgb within 1e-2, gradients within 1e-2), against oracle
 loss) and the reference's ops in float64 (gradients, tests/test_gpu_parity.py _compare_step):
   * rgb <= 1e-2 abs (measured <= 2.8e-5: the single fp16 activation and the fp16 hi + lo weights);
   * every MLP gradient within 1e-2 of its max (measured 2.2e-3), cosine >= 0.999;
-  * d warp cosine >= 0.999 and error <= max(1e-2, 10 x the reference's own fp32 error): d warp is
+  * d warp cosine >= 0.999 and error <= max(1e-2, 10 x the reference's own fp32 error) (measured
+    2.5e-2 / 3.6e-2 at c3x2 / c3x3 against the reference's 5.3e-3 / 4.2e-3; 3.2e-3 at c1): d warp is
     a sum over 10^5 pixels that cancels, and the fp16 forward's rgb error is smooth over the image
     (correlated, not averaged out), so its share of the cancelled sum is larger than the split-bf16
     recipe's (measured in an emulation of the recipes in the fp32 kernels, tools/emu_grad_err.py,
@@ -48,6 +49,7 @@ def test_fp16x2_step_vs_oracle(shape, tmp_path):
     m, var, inputs = _synthetic_setup("fp16x2", tmp_path, *SHAPES[shape])
     assert m.graph.neural_image.engine(torch.device(DEV)).net.step_kernel == "k_step2h"
     o = _compare_step(m, var, inputs, "fp16x2", 5)
+    print(shape, {k: float(f"{v:.3g}") for k, v in o.items() if isinstance(v, float)})
     assert o["rgb"] <= 1e-2 and o["loss"] <= 1e-2, o
     assert o["grad_err"] <= 1e-2 and o["grad_cos"] >= 0.999, o
     assert o["dh_err"] <= max(1e-2, 10 * o["dh_err_ref32"]) and o["dh_cos"] >= 0.999, o
