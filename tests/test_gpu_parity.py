@@ -1149,6 +1149,21 @@ def test_c3_two_patch_step_vs_oracle(precision, tmp_path):
         assert o["grad_err"] <= 2 * o["grad_err_ref32"] and o["dh_err"] <= 2 * o["dh_err_ref32"], o
 
 
+@pytest.mark.parametrize("c2f,progress", [(None, 0.2), ((0, 0.4), 0.0), ((0, 0.4), 1.0)])
+def test_bf16x3_step_c2f_settings(c2f, progress, tmp_path):
+    """The benchmarked recipe with the band weights at their extremes (c2f off, every band masked,
+    every band open) on 3 patches of 128^2 with the C1 net, against the reference's ops in float64:
+    rgb <= 1e-5, MLP gradients and d warp within the bf16 1e-2 of their max at cosine >= 0.9999
+    (measured: d warp 3.5e-3 / 1.1e-3 / 3.8e-3, the reference's own fp32 1.9e-3 / 2e-6 / 3.4e-3;
+    profiles/r8n/c2f_probe.log)."""
+    m, var, inputs = _synthetic_setup("bf16x3", tmp_path, 3, 128, 8, [256] * 4, c2f=c2f, progress=progress)
+    o = _compare_step(m, var, inputs, "bf16x3", 5)
+    print(c2f, progress, {k: float(f"{v:.3g}") for k, v in o.items() if isinstance(v, float)})
+    assert o["rgb"] <= 1e-5 and o["loss"] <= 1e-5, o
+    assert o["grad_err"] <= 1e-2 and o["grad_cos"] >= 0.9999, o
+    assert o["dh_err"] <= 1e-2 and o["dh_cos"] >= 0.9999, o
+
+
 @pytest.mark.parametrize("shape", ["c3x2", "c1", "narrow"])
 def test_bf16x3_split_dz_step(shape, tmp_path, monkeypatch):
     """The split recipe with the dgrad's dz split too (MARF_STEP2_DZ=1 at net creation: k_step2dz,
