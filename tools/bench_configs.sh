@@ -8,7 +8,7 @@ OUT=$PWD/gpurun_out/$TAG
 mkdir -p $OUT
 run() {
   local name=$1; shift
-  timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "$name failed"; tail -3 $OUT/$name.err; return 1; }
+  timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-alt-recipe "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "$name failed"; tail -3 $OUT/$name.err; return 1; }
   python - $OUT/$name.json $name <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
